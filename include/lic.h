@@ -1,0 +1,197 @@
+/*
+ * lic.h — C ABI of liblic.so, the MI355X (gfx950) kernels behind the
+ * encode -> quantize -> decode hot path of the learned image codec
+ * (reference: xiaobucc/learning-driven-image-compression-algorithm).
+ *
+ * The reference has no native plugin/FFI layer: its boundary is the PyTorch
+ * nn.Module surface.  Every entry point below replaces the
+ * L0 PyTorch op sequence of one reference layer, cited per function.  The
+ * Python host modules in lic_amd/ (same class names and state_dict keys as the
+ * reference) call these through ctypes (lic_amd/_ffi.py); INTEGRATION.md shows
+ * the binding.
+ *
+ * Conventions
+ *  - Activations are NHWC ("pixel-major", channels contiguous).  A view is
+ *    (data, n, h, w, c, ld): `data` already points at the first channel of the
+ *    view, `ld` is the element stride between consecutive pixels, so channel
+ *    slices / concatenations (torch.cat, torch.split, chunk) are free.
+ *  - dtype tag: LIC_F32 or LIC_F16 for activations and packed weights; biases,
+ *    GDN/LayerNorm parameters, scales and metrics are always fp32.
+ *  - All tensors are caller-owned device memory; the library never allocates,
+ *    frees or retains.  Calls are asynchronous on the given stream and are safe
+ *    under stream capture (hipGraph).  Errors: non-zero status +
+ *    lic_last_error() (thread-local message).
+ */
+#ifndef LIC_H_
+#define LIC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* lic_stream_t; /* hipStream_t */
+
+enum lic_dtype { LIC_F32 = 0, LIC_F16 = 1 };
+enum lic_act { LIC_ACT_NONE = 0, LIC_ACT_RELU = 1, LIC_ACT_LRELU = 2, LIC_ACT_GELU = 3, LIC_ACT_ROUND = 4 };
+enum lic_prologue { LIC_PRO_NONE = 0, LIC_PRO_SQUARE = 1, LIC_PRO_ABS = 2 };
+enum lic_epilogue {
+  LIC_EPI_PLAIN = 0,     /* v = act(acc+bias) (+ r1)                                  */
+  LIC_EPI_GATE = 1,      /* v = g * sigmoid(act(acc+bias) (+ r1)) + r2   (WNSA / SWAtten) */
+  LIC_EPI_HALF_TANH = 2, /* v = r2 + 0.5*tanh(act(acc+bias))             (LRP)           */
+  LIC_EPI_GDN_DIV = 3,   /* v = g / sqrt(acc+beta) (+ r1)      model/gdn.py GDN          */
+  LIC_EPI_GDN_RSQRT = 4, /* v = g * rsqrt(acc+beta) (+ r1)     layers/gdn.py GDN          */
+  LIC_EPI_GDN_SQRT = 5,  /* v = g * sqrt(acc+beta) (+ r1)      IGDN (both variants)       */
+  LIC_EPI_RES_ACT = 6    /* v = act(acc+bias+r1)               compressai ResidualUnit    */
+};
+
+#define LIC_MAX_TAPS 64
+
+/* One convolution launch in "tap" form.
+ *   out[b, oy0 + osy*i, ox0 + osx*j, n]  for i < mi, j < mj, n < co
+ *     = epilogue( bias[n] + sum_t sum_c pro(x[b, i*isy + dy[t], j*isx + dx[t], c]) * w[n][t][c] )
+ * with x zero outside [0,h)x[0,w).  A standard conv (stride s, pads pt/pl) is
+ * isy=isx=s, dy=ky-pt, dx=kx-pl; a transposed conv is up to s*s such launches,
+ * one per output phase (sub-pixel decomposition).  w is packed
+ * [copad][ntaps][cpad] in `dtype`, zero-padded (copad >= co, cpad >= ci/groups).
+ * out_shuffle=2 writes channel n of pixel (y,x) to channel n/4 of pixel
+ * (2y + (n>>1&1), 2x + (n&1)) (conv + nn.PixelShuffle(2)).                    */
+typedef struct lic_conv_args {
+  int32_t dtype;
+  /* input view */
+  const void* x; int32_t n, h, w, ci, ldx;
+  /* output view (h, w are the full output map) */
+  void* y; int32_t ho, wo, co, ldy;
+  void* y2; int32_t ldy2;            /* optional second destination (same values) */
+  /* lattice */
+  int32_t mi, mj, oy0, ox0, osy, osx, isy, isx;
+  int32_t ntaps; int8_t dy[LIC_MAX_TAPS]; int8_t dx[LIC_MAX_TAPS];
+  int32_t groups;                    /* 1, or ci for depthwise (direct kernel only) */
+  /* weights */
+  const void* wgt; int32_t cpad, copad;
+  const float* bias;                 /* may be NULL */
+  /* prologue / epilogue */
+  int32_t prologue;                  /* lic_prologue, applied to x values */
+  int32_t act; float slope;
+  int32_t epi;
+  const void* r1; int32_t ldr1;      /* views with the output's pixel geometry */
+  const void* g;  int32_t ldg;
+  const void* r2; int32_t ldr2;
+  int32_t out_shuffle;               /* 0 or 2 */
+  int32_t force_direct;              /* testing: force the non-MFMA kernel */
+} lic_conv_args;
+
+/* Convolution / linear layer (nn.Conv2d, nn.ConvTranspose2d phase, nn.Linear as
+ * 1x1) with fused epilogue.  Replaces F.conv2d + activation + residual chains,
+ * e.g. net_ga.py:89-103 (ResidualBottleneck), layers/layers.py:36-54,105-111,
+ * compressai ResidualBlock/ResidualBlockWithStride/AttentionBlock, and
+ * F.conv2d(x**2, gamma, beta) + x*rsqrt/sqrt of layers/gdn.py:62-75 /
+ * model/gdn.py:69-92 (prologue SQUARE + GDN epilogues).                        */
+int lic_conv2d_fwd(const lic_conv_args* a, lic_stream_t stream);
+
+/* GDN parameter reparametrisation: beta' = max(beta,beta_bound)^2 - pedestal,
+ * gamma' = max(gamma,gamma_bound)^2 - pedestal, written as packed conv weight
+ * [copad][1][cpad] (dtype) and fp32 bias.  model/gdn.py:69-84 (LowerBound
+ * :11-28, evaluated on device — no per-call host tensor) and
+ * ops/parametrizers.py:48-51 + ops/bound_ops.py:40-41.                          */
+int lic_gdn_prepare(int32_t dtype, const float* beta, const float* gamma, int32_t c,
+                    float beta_bound, float gamma_bound, float pedestal,
+                    void* wgt_out, int32_t cpad, int32_t copad, float* beta_out,
+                    lic_stream_t stream);
+
+/* Shifted-window multi-head self-attention core over a qkv view (3C channels,
+ * q|k|v, head-major inside each): roll(-shift) + window_partition + (q*scale)k^T
+ * (or (qk^T)*scale) + relative-position bias + mask + softmax + AV +
+ * window_reverse + roll(+shift).  Output view has C channels at the original
+ * pixel positions (the proj Linear + residual is a following conv launch).
+ *   WBA  (layers/win_attention.py:85-116,154-209): scale_after=0, mask_kind=1 (-100)
+ *   WMSA (model/Block_unet.py:216-252):           scale_after=1, mask_kind=2 (-inf)
+ * Bias table element (r = dy*(2ws-1)+dx, head h) at table[r*tab_sr + h*tab_sh]. */
+typedef struct lic_attn_args {
+  int32_t dtype;
+  const void* qkv; int32_t n, h, w, c, ldqkv;
+  void* out; int32_t ldo;
+  int32_t heads, ws, shift;
+  const float* table; int32_t tab_sr, tab_sh;
+  int32_t mask_kind;   /* 0 none, 1 WBA regions (-100), 2 WMSA last row/col (-inf) */
+  int32_t scale_after; /* 0: q*scale before dot, 1: dot*scale */
+  float scale;         /* head_dim ** -0.5 (as the reference's Python float, cast to fp32) */
+} lic_attn_args;
+int lic_win_attn_fwd(const lic_attn_args* a, lic_stream_t stream);
+
+/* LayerNorm over channels (nn.LayerNorm(C), eps) per pixel.  net_ga.py:115-127. */
+int lic_layernorm_fwd(int32_t dtype, const void* x, int32_t npix, int32_t c, int32_t ldx,
+                      const float* weight, const float* bias, float eps,
+                      void* y, int32_t ldy, lic_stream_t stream);
+
+/* Gaussian-conditional quantisation + rate for one slice (compressai
+ * GaussianConditional in 'dequantize' mode at net_ga.py:1049, ste_round at :1053):
+ *   q = rint(y - mu)           -> symbols (int32, may be NULL)
+ *   yq = q + mu                -> yq / yq2 (dtype views, may be NULL)
+ *   L  = max(Phi((.5-|yq-mu|)/s) - Phi((-.5-|yq-mu|)/s), 1e-9), s = max(scale, .11)
+ *   partial[blockIdx] = sum ln L (fp64), nblocks written to *nparts.            */
+typedef struct lic_rate_args {
+  int32_t dtype;
+  int32_t npix, c;
+  const void* y; int32_t ldy;
+  const void* mu; int32_t ldmu;
+  const void* scale; int32_t ldsc;
+  void* yq; int32_t ldyq;
+  void* yq2; int32_t ldyq2;
+  int32_t* symbols; int32_t ldsym;
+  float* likelihood; int32_t ldlik;  /* fp32 view, may be NULL */
+  double* partials; int32_t max_parts;
+  float scale_bound, likelihood_bound;
+} lic_rate_args;
+int lic_gauss_rate_fwd(const lic_rate_args* a, lic_stream_t stream);
+
+/* z_hat = round(z - m[c]) + m[c] (EntropyBottleneck._get_medians path,
+ * net_ga.py:996-1003).  Also used for ste/bypass rounding with m = NULL. */
+int lic_quantize_median(int32_t dtype, const void* z, int32_t npix, int32_t c, int32_t ldz,
+                        const float* medians, void* out, int32_t ldo, lic_stream_t stream);
+
+/* Sum of fp64 partials -> bpp = sum / (-ln2 * num_pixels) written as fp32 [1]
+ * and fp64 [1] (net_ga.py:1134). */
+int lic_bpp_finalize(const double* partials, int32_t nparts, double num_pixels,
+                     float* bpp_out, double* sum_out, lic_stream_t stream);
+
+/* Syntax-generated per-image 1x1 head + tanh + clamp + 8-bit metrics:
+ * net_ga.py:969-979 (batch_conv), :1092 (tanh), :1118 (clamp), :1137-1142.
+ *   xt[b,o] = clamp(tanh(sum_c wgen[b*ldw + o*cin + c] * xtil[b,pix,c]), -1, 1)  (wgen in dtype)
+ *   sqerr_partial[b][blk] = sum (round(clamp((xt+1)*127.5,0,255)) - round((x+1)*127.5))^2
+ * x (reference input) and x_rec are NCHW fp32 [n,3,h,w]; xtil is an NHWC view. */
+int lic_syntax_recon_fwd(int32_t dtype, const void* xtil, int32_t n, int32_t h, int32_t w,
+                         int32_t cin, int32_t ldx, const void* wgen, int32_t ldw, const float* x,
+                         float* x_rec, double* sqerr_partials, int32_t parts_per_img,
+                         lic_stream_t stream);
+/* v_mse[b] = sum/(3hw); v_psnr = mean_b 20 log10(255/sqrt(v_mse[b])). */
+int lic_psnr_finalize(const double* sqerr_partials, int32_t n, int32_t parts_per_img,
+                      double count, float* v_mse, float* v_psnr, lic_stream_t stream);
+
+/* Layout / elementwise helpers. */
+/* NCHW fp32 -> NHWC view of dtype (and back). */
+int lic_nchw_to_nhwc(int32_t dtype, const float* x, int32_t n, int32_t c, int32_t h, int32_t w,
+                     void* y, int32_t ldy, lic_stream_t stream);
+int lic_nhwc_to_nchw(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t c,
+                     int32_t ldx, float* y, lic_stream_t stream);
+/* y = a + b (views, same geometry). */
+int lic_add(int32_t dtype, const void* a, int32_t lda, const void* b, int32_t ldb, int32_t npix,
+            int32_t c, void* y, int32_t ldy, lic_stream_t stream);
+/* Copy a view (optionally casting dtype). */
+int lic_copy(int32_t dtype_in, const void* x, int32_t ldx, int32_t npix, int32_t c,
+             int32_t dtype_out, void* y, int32_t ldy, lic_stream_t stream);
+/* Adaptive average pool to 1x1 (nn.AdaptiveAvgPool2d(1)) into a dtype row
+ * y[b*ldy + c] (fp32 accumulation). */
+int lic_avgpool(int32_t dtype, const void* x, int32_t n, int32_t hw, int32_t c, int32_t ldx,
+                void* y, int32_t ldy, lic_stream_t stream);
+
+/* Library info. */
+const char* lic_last_error(void);
+const char* lic_version(void);
+int lic_device_arch(char* buf, int32_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIC_H_ */

@@ -1,0 +1,160 @@
+// Layout conversion and small elementwise / pooling helpers (gfx950).
+#include "lic_common.h"
+
+namespace lic {
+
+// NCHW fp32 -> NHWC view (dtype T). One thread per output element, reads
+// coalesced along w for each channel plane via a 2-D grid.
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int n, int c, int h, int w, T* __restrict__ y,
+                                    int ldy) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)n * c * h * w;
+  if (idx >= total) return;
+  // idx enumerates NHWC order: ((b*h + yy)*w + xx)*c + k
+  const int k = (int)(idx % c);
+  const int64_t pix = idx / c;
+  const int xx = (int)(pix % w);
+  const int64_t t = pix / w;
+  const int yy = (int)(t % h);
+  const int b = (int)(t / h);
+  y[pix * ldy + k] = from_f<T>(x[(((int64_t)b * c + k) * h + yy) * w + xx]);
+}
+
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(const T* __restrict__ x, int n, int h, int w, int c, int ldx, float* __restrict__ y) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)n * c * h * w;
+  if (idx >= total) return;
+  // idx enumerates NCHW order
+  const int xx = (int)(idx % w);
+  int64_t t = idx / w;
+  const int yy = (int)(t % h);
+  t /= h;
+  const int k = (int)(t % c);
+  const int b = (int)(t / c);
+  y[idx] = to_f(x[(((int64_t)b * h + yy) * w + xx) * ldx + k]);
+}
+
+template <typename T>
+__global__ void add_kernel(const T* __restrict__ a, int lda, const T* __restrict__ b, int ldb, int npix, int c,
+                           T* __restrict__ y, int ldy) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)npix * c) return;
+  const int64_t p = idx / c;
+  const int k = (int)(idx - p * c);
+  y[p * ldy + k] = from_f<T>(to_f(a[p * lda + k]) + to_f(b[p * ldb + k]));
+}
+
+template <typename TI, typename TO>
+__global__ void copy_kernel(const TI* __restrict__ x, int ldx, int npix, int c, TO* __restrict__ y, int ldy) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)npix * c) return;
+  const int64_t p = idx / c;
+  const int k = (int)(idx - p * c);
+  y[p * ldy + k] = from_f<TO>(to_f(x[p * ldx + k]));
+}
+
+// AdaptiveAvgPool2d(1): one block per (image, 64-channel group); threads stride pixels.
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_kernel(const T* __restrict__ x, int hw, int c, int ldx,
+                                                      T* __restrict__ y, int ldy) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.y;
+  const int k = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  float s = 0.f;
+  if (k < c)
+    for (int p = part; p < hw; p += 4) s += to_f(x[((int64_t)b * hw + p) * ldx + k]);
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && k < c) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    y[(int64_t)b * ldy + k] = from_f<T>(t / (float)hw);
+  }
+}
+
+}  // namespace lic
+
+using namespace lic;
+
+#define DISPATCH_T(dtype, NAME, ...)                                   \
+  do {                                                                 \
+    if ((dtype) == LIC_F32) {                                          \
+      typedef float T;                                                 \
+      __VA_ARGS__;                                                     \
+    } else if ((dtype) == LIC_F16) {                                   \
+      typedef half_t T;                                                \
+      __VA_ARGS__;                                                     \
+    } else                                                             \
+      return fail(std::string(NAME) + ": bad dtype");                  \
+  } while (0)
+
+static inline unsigned nblk(int64_t total) { return (unsigned)((total + 255) / 256); }
+
+extern "C" int lic_nchw_to_nhwc(int32_t dtype, const float* x, int32_t n, int32_t c, int32_t h, int32_t w, void* y,
+                                int32_t ldy, lic_stream_t stream) {
+  const int64_t total = (int64_t)n * c * h * w;
+  if (!total) return 0;
+  DISPATCH_T(dtype, "nchw_to_nhwc",
+             hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, x, n, c,
+                                h, w, (T*)y, ldy));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_nhwc_to_nchw(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ldx,
+                                float* y, lic_stream_t stream) {
+  const int64_t total = (int64_t)n * c * h * w;
+  if (!total) return 0;
+  DISPATCH_T(dtype, "nhwc_to_nchw",
+             hipLaunchKernelGGL(nhwc_to_nchw_kernel<T>, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream,
+                                (const T*)x, n, h, w, c, ldx, y));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_add(int32_t dtype, const void* a, int32_t lda, const void* b, int32_t ldb, int32_t npix, int32_t c,
+                       void* y, int32_t ldy, lic_stream_t stream) {
+  const int64_t total = (int64_t)npix * c;
+  if (!total) return 0;
+  DISPATCH_T(dtype, "add",
+             hipLaunchKernelGGL(add_kernel<T>, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, (const T*)a, lda,
+                                (const T*)b, ldb, npix, c, (T*)y, ldy));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_copy(int32_t dtype_in, const void* x, int32_t ldx, int32_t npix, int32_t c, int32_t dtype_out,
+                        void* y, int32_t ldy, lic_stream_t stream) {
+  const int64_t total = (int64_t)npix * c;
+  if (!total) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == LIC_F32 && dtype_out == LIC_F32)
+    hipLaunchKernelGGL((copy_kernel<float, float>), dim3(nblk(total)), dim3(256), 0, s, (const float*)x, ldx, npix, c,
+                       (float*)y, ldy);
+  else if (dtype_in == LIC_F32 && dtype_out == LIC_F16)
+    hipLaunchKernelGGL((copy_kernel<float, half_t>), dim3(nblk(total)), dim3(256), 0, s, (const float*)x, ldx, npix, c,
+                       (half_t*)y, ldy);
+  else if (dtype_in == LIC_F16 && dtype_out == LIC_F32)
+    hipLaunchKernelGGL((copy_kernel<half_t, float>), dim3(nblk(total)), dim3(256), 0, s, (const half_t*)x, ldx, npix,
+                       c, (float*)y, ldy);
+  else if (dtype_in == LIC_F16 && dtype_out == LIC_F16)
+    hipLaunchKernelGGL((copy_kernel<half_t, half_t>), dim3(nblk(total)), dim3(256), 0, s, (const half_t*)x, ldx, npix,
+                       c, (half_t*)y, ldy);
+  else
+    return fail("copy: bad dtype");
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_avgpool(int32_t dtype, const void* x, int32_t n, int32_t hw, int32_t c, int32_t ldx, void* y,
+                           int32_t ldy, lic_stream_t stream) {
+  if (!n || !c) return 0;
+  dim3 grid((c + 63) / 64, n);
+  DISPATCH_T(dtype, "avgpool",
+             hipLaunchKernelGGL(avgpool_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)x, hw, c, ldx, (T*)y,
+                                ldy));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,383 @@
+"""Tensor-level wrappers around liblic (NHWC activation views, packed weights).
+
+``Act`` is an NHWC view (tensor [B, H, W, Ctot] contiguous + channel window), so
+channel slices and concatenations are free: producers write straight into the
+consumer's concat buffer.  All ops enqueue on the current torch stream and never
+synchronise.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _ffi
+from ._ffi import ConvArgs, AttnArgs, RateArgs, check
+
+_DT = {torch.float32: _ffi.LIC_F32, torch.float16: _ffi.LIC_F16}
+
+
+def dtype_id(dt: torch.dtype) -> int:
+    try:
+        return _DT[dt]
+    except KeyError:
+        raise _ffi.LicError(f"unsupported activation dtype {dt}; use float32 or float16")
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _lib():
+    return _ffi.load()
+
+
+class Act:
+    """NHWC activation view: channels [c0, c0 + c) of a contiguous [B, H, W, Ctot] tensor."""
+    __slots__ = ("t", "c0", "c")
+
+    def __init__(self, t: torch.Tensor, c0: int = 0, c: Optional[int] = None):
+        if t.dim() != 4 or not t.is_contiguous():
+            raise ValueError("Act expects a contiguous [B, H, W, C] tensor")
+        self.t = t
+        self.c0 = c0
+        self.c = t.shape[3] - c0 if c is None else c
+
+    @property
+    def B(self):
+        return self.t.shape[0]
+
+    @property
+    def H(self):
+        return self.t.shape[1]
+
+    @property
+    def W(self):
+        return self.t.shape[2]
+
+    @property
+    def ld(self):
+        return self.t.shape[3]
+
+    @property
+    def npix(self):
+        return self.t.shape[0] * self.t.shape[1] * self.t.shape[2]
+
+    @property
+    def ptr(self):
+        return self.t.data_ptr() + self.c0 * self.t.element_size()
+
+    @property
+    def dtype(self):
+        return self.t.dtype
+
+    def ch(self, a: int, b: int) -> "Act":
+        assert 0 <= a <= b <= self.c
+        return Act(self.t, self.c0 + a, b - a)
+
+    def nchw(self) -> torch.Tensor:
+        """Logical NCHW tensor (channels_last storage) of this view."""
+        v = self.t[..., self.c0:self.c0 + self.c]
+        return v.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def empty(B, H, W, C, dtype, device) -> "Act":
+        return Act(torch.empty((B, H, W, C), dtype=dtype, device=device))
+
+    @staticmethod
+    def from_nchw(x: torch.Tensor, dtype: Optional[torch.dtype] = None) -> "Act":
+        """NCHW-logical tensor -> NHWC Act (zero copy when already channels_last of the dtype)."""
+        dtype = dtype or x.dtype
+        t = x.permute(0, 2, 3, 1)
+        if t.dtype == dtype and t.is_contiguous():
+            return Act(t)
+        if x.dtype == torch.float32 and x.is_contiguous():
+            B, C, H, W = x.shape
+            out = Act.empty(B, H, W, C, dtype, x.device)
+            check(_lib().lic_nchw_to_nhwc(dtype_id(dtype), x.data_ptr(), B, C, H, W, out.ptr, out.ld,
+                                          stream_handle()))
+            return out
+        return Act(t.to(dtype).contiguous())
+
+
+# --------------------------------------------------------------------------- packed convolutions
+@dataclass
+class ConvPack:
+    """One conv launch's packed weights and tap geometry."""
+    w: torch.Tensor                 # [copad, ntaps, cpad] in activation dtype
+    bias: Optional[torch.Tensor]    # fp32 [co]
+    ci: int
+    co: int
+    dy: List[int]
+    dx: List[int]
+    groups: int = 1
+    # lattice (None -> standard conv computed from stride/pad)
+    stride: int = 1
+    pad: Tuple[int, int, int, int] = (0, 0, 0, 0)  # top, left, bottom, right
+    kh: int = 1
+    kw: int = 1
+    phase: Optional[Tuple[int, int, int, int, int]] = None  # (oy0, ox0, osy, osx, dummy) for convT phases
+
+    @property
+    def cpad(self):
+        return self.w.shape[2]
+
+    @property
+    def copad(self):
+        return self.w.shape[0]
+
+
+def _choose_copad(co: int) -> int:
+    best, best_cost = None, None
+    for bn in (192, 128, 96, 64, 32):
+        nb = -(-co // bn)
+        cost = nb * bn * (1 + 0.05 * nb)
+        if best_cost is None or cost < best_cost - 1e-9:
+            best, best_cost = nb * bn, cost
+    return best
+
+
+def _cpad_for(ci: int, dtype: torch.dtype) -> int:
+    bk = 32 if dtype == torch.float16 else 16
+    return -(-ci // bk) * bk
+
+
+def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad, dtype: torch.dtype,
+                groups: int = 1) -> ConvPack:
+    """nn.Conv2d weight [co, ci/g, kh, kw] -> packed [copad][kh*kw][cpad]; pad = (top, left, bottom, right)."""
+    co, cig, kh, kw = weight.shape
+    pt, pl, pb, pr = pad
+    cpad = _cpad_for(cig, dtype) if groups == 1 else cig
+    copad = _choose_copad(co)
+    w = torch.zeros((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
+    w[:co, :, :cig] = weight.detach().permute(0, 2, 3, 1).reshape(co, kh * kw, cig).to(dtype)
+    dy = [ky - pt for ky in range(kh) for kx in range(kw)]
+    dx = [kx - pl for ky in range(kh) for kx in range(kw)]
+    b = bias.detach().float().contiguous() if bias is not None else None
+    return ConvPack(w=w, bias=b, ci=cig * groups, co=co, dy=dy, dx=dx, groups=groups, stride=stride,
+                    pad=(pt, pl, pb, pr), kh=kh, kw=kw)
+
+
+def pack_conv_transpose2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
+                          output_padding: int, dtype: torch.dtype, prepad: Tuple[int, int] = (0, 0)) -> List[ConvPack]:
+    """nn.ConvTranspose2d weight [ci, co, kh, kw] (optionally after ZeroPad2d(top=prepad[0],
+    left=prepad[1])) -> one ConvPack per output phase (sub-pixel decomposition, gather form)."""
+    ci, co, kh, kw = weight.shape
+    s, p = stride, padding
+    packs = []
+    wt = weight.detach()
+    for ry in range(s):
+        for rx in range(s):
+            kys = [ky for ky in range(kh) if (ry + p - ky) % s == 0]
+            kxs = [kx for kx in range(kw) if (rx + p - kx) % s == 0]
+            taps = [(ky, kx) for ky in kys for kx in kxs]
+            if not taps:
+                continue
+            cpad = _cpad_for(ci, dtype)
+            copad = _choose_copad(co)
+            w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
+            for t, (ky, kx) in enumerate(taps):
+                w[:co, t, :ci] = wt[:, :, ky, kx].t().to(dtype)
+            dy = [(ry + p - ky) // s - prepad[0] for ky, kx in taps]
+            dx = [(rx + p - kx) // s - prepad[1] for ky, kx in taps]
+            b = bias.detach().float().contiguous() if bias is not None else None
+            packs.append(ConvPack(w=w, bias=b, ci=ci, co=co, dy=dy, dx=dx, kh=kh, kw=kw, stride=s,
+                                  phase=(ry, rx, s, s, 0)))
+    return packs
+
+
+def conv_out_hw(H, W, pk: ConvPack):
+    pt, pl, pb, pr = pk.pad
+    return (H + pt + pb - pk.kh) // pk.stride + 1, (W + pl + pr - pk.kw) // pk.stride + 1
+
+
+def convT_out_hw(H, W, stride, padding, output_padding, k, prepad=(0, 0)):
+    Hp, Wp = H + prepad[0], W + prepad[1]
+    return (Hp - 1) * stride - 2 * padding + k + output_padding, (Wp - 1) * stride - 2 * padding + k + output_padding
+
+
+def _ptr(a: Optional[Act]):
+    return (a.ptr, a.ld) if a is not None else (None, 0)
+
+
+def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT_NONE, slope: float = 0.01,
+         epi: int = _ffi.EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
+         y2: Optional[Act] = None, prologue: int = _ffi.PRO_NONE, out_hw=None, shuffle: bool = False,
+         force_direct: bool = False) -> Act:
+    """Run one ConvPack launch. For convT phases `out` (full map) must be given."""
+    if x.c != pk.ci:
+        raise ValueError(f"conv: input has {x.c} channels, weights expect {pk.ci}")
+    if pk.w.dtype != x.dtype:
+        raise ValueError("conv: packed weight dtype != activation dtype")
+    if pk.phase is None:
+        Ho, Wo = out_hw if out_hw is not None else conv_out_hw(x.H, x.W, pk)
+        mi, mj, oy0, ox0, osy, osx, isy, isx = Ho, Wo, 0, 0, 1, 1, pk.stride, pk.stride
+    else:
+        if out is None:
+            raise ValueError("conv: transposed-conv phase needs the output view")
+        ry, rx, s, _, _ = pk.phase
+        Ho, Wo = out.H, out.W
+        mi, mj = -(-(Ho - ry) // s), -(-(Wo - rx) // s)
+        oy0, ox0, osy, osx, isy, isx = ry, rx, s, s, 1, 1
+    if out is None:
+        if shuffle:
+            out = Act.empty(x.B, Ho * 2, Wo * 2, pk.co // 4, x.dtype, x.t.device)
+        else:
+            out = Act.empty(x.B, Ho, Wo, pk.co, x.dtype, x.t.device)
+    a = ConvArgs()
+    a.dtype = dtype_id(x.dtype)
+    a.x, a.n, a.h, a.w, a.ci, a.ldx = x.ptr, x.B, x.H, x.W, x.c, x.ld
+    a.y, a.ho, a.wo, a.co, a.ldy = out.ptr, out.H, out.W, pk.co, out.ld
+    if shuffle:
+        a.ho, a.wo = out.H, out.W
+    a.y2, a.ldy2 = _ptr(y2)
+    a.mi, a.mj, a.oy0, a.ox0, a.osy, a.osx, a.isy, a.isx = mi, mj, oy0, ox0, osy, osx, isy, isx
+    nt = len(pk.dy)
+    a.ntaps = nt
+    for t in range(nt):
+        a.dy[t] = pk.dy[t]
+        a.dx[t] = pk.dx[t]
+    a.groups = pk.groups
+    a.wgt, a.cpad, a.copad = pk.w.data_ptr(), pk.cpad, pk.copad
+    a.bias = pk.bias.data_ptr() if pk.bias is not None else None
+    a.prologue, a.act, a.slope, a.epi = prologue, act, slope, epi
+    a.r1, a.ldr1 = _ptr(r1)
+    a.g, a.ldg = _ptr(g)
+    a.r2, a.ldr2 = _ptr(r2)
+    a.out_shuffle = 2 if shuffle else 0
+    a.force_direct = 1 if force_direct else 0
+    check(_lib().lic_conv2d_fwd(ctypes.byref(a), stream_handle()))
+    return out
+
+
+def conv_transpose(x: Act, packs: Sequence[ConvPack], Ho: int, Wo: int, out: Optional[Act] = None, **kw) -> Act:
+    if out is None:
+        out = Act.empty(x.B, Ho, Wo, packs[0].co, x.dtype, x.t.device)
+    for pk in packs:
+        conv(x, pk, out, **kw)
+    return out
+
+
+# --------------------------------------------------------------------------- other ops
+def gdn_prepare(beta: torch.Tensor, gamma: torch.Tensor, beta_bound: float, gamma_bound: float, pedestal: float,
+                dtype: torch.dtype) -> ConvPack:
+    C = beta.shape[0]
+    cpad = _cpad_for(C, dtype)
+    copad = _choose_copad(C)
+    w = torch.empty((copad, 1, cpad), dtype=dtype, device=beta.device)
+    b = torch.empty((C,), dtype=torch.float32, device=beta.device)
+    check(_lib().lic_gdn_prepare(dtype_id(dtype), beta.detach().float().contiguous().data_ptr(),
+                                 gamma.detach().float().contiguous().data_ptr(), C, beta_bound, gamma_bound,
+                                 pedestal, w.data_ptr(), cpad, copad, b.data_ptr(), stream_handle()))
+    return ConvPack(w=w, bias=b, ci=C, co=C, dy=[0], dx=[0])
+
+
+def gdn(x: Act, pk: ConvPack, mode: int, out: Optional[Act] = None, r1: Optional[Act] = None) -> Act:
+    """mode: EPI_GDN_DIV (model/gdn GDN), EPI_GDN_RSQRT (compressai GDN), EPI_GDN_SQRT (IGDN)."""
+    return conv(x, pk, out, epi=mode, g=x, r1=r1, prologue=_ffi.PRO_SQUARE)
+
+
+def win_attn(qkv: Act, C: int, heads: int, ws: int, shift: int, table: torch.Tensor, tab_sr: int, tab_sh: int,
+             mask_kind: int, scale_after: bool, scale: float, out: Optional[Act] = None) -> Act:
+    if out is None:
+        out = Act.empty(qkv.B, qkv.H, qkv.W, C, qkv.dtype, qkv.t.device)
+    a = AttnArgs()
+    a.dtype = dtype_id(qkv.dtype)
+    a.qkv, a.n, a.h, a.w, a.c, a.ldqkv = qkv.ptr, qkv.B, qkv.H, qkv.W, C, qkv.ld
+    a.out, a.ldo = out.ptr, out.ld
+    a.heads, a.ws, a.shift = heads, ws, shift
+    a.table, a.tab_sr, a.tab_sh = table.data_ptr(), tab_sr, tab_sh
+    a.mask_kind, a.scale_after, a.scale = mask_kind, 1 if scale_after else 0, scale
+    check(_lib().lic_win_attn_fwd(ctypes.byref(a), stream_handle()))
+    return out
+
+
+def layernorm(x: Act, weight: torch.Tensor, bias: torch.Tensor, eps: float, out: Optional[Act] = None) -> Act:
+    if out is None:
+        out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)
+    check(_lib().lic_layernorm_fwd(dtype_id(x.dtype), x.ptr, x.npix, x.c, x.ld, weight.data_ptr(), bias.data_ptr(),
+                                   eps, out.ptr, out.ld, stream_handle()))
+    return out
+
+
+def add(a: Act, b: Act, out: Optional[Act] = None) -> Act:
+    if out is None:
+        out = Act.empty(a.B, a.H, a.W, a.c, a.dtype, a.t.device)
+    check(_lib().lic_add(dtype_id(a.dtype), a.ptr, a.ld, b.ptr, b.ld, a.npix, a.c, out.ptr, out.ld, stream_handle()))
+    return out
+
+
+def copy(x: Act, out: Act) -> Act:
+    check(_lib().lic_copy(dtype_id(x.dtype), x.ptr, x.ld, x.npix, x.c, dtype_id(out.dtype), out.ptr, out.ld,
+                          stream_handle()))
+    return out
+
+
+def avgpool(x: Act, out: Act) -> Act:
+    """AdaptiveAvgPool2d(1): out is a [B, 1, 1, C] view."""
+    check(_lib().lic_avgpool(dtype_id(x.dtype), x.ptr, x.B, x.H * x.W, x.c, x.ld, out.ptr, out.ld,
+                             stream_handle()))
+    return out
+
+
+def quantize_median(z: Act, medians: Optional[torch.Tensor], out: Optional[Act] = None) -> Act:
+    if out is None:
+        out = Act.empty(z.B, z.H, z.W, z.c, z.dtype, z.t.device)
+    check(_lib().lic_quantize_median(dtype_id(z.dtype), z.ptr, z.npix, z.c, z.ld,
+                                     medians.data_ptr() if medians is not None else None,
+                                     out.ptr, out.ld, stream_handle()))
+    return out
+
+
+def gauss_rate(y: Act, mu: Act, scale: Act, partials: torch.Tensor, part_off: int, *, yq: Optional[Act] = None,
+               yq2: Optional[Act] = None, symbols: Optional[Act] = None, likelihood: Optional[Act] = None,
+               scale_bound: float = 0.11, likelihood_bound: float = 1e-9) -> int:
+    """Returns the number of partials written at partials[part_off:]."""
+    a = RateArgs()
+    a.dtype = dtype_id(y.dtype)
+    a.npix, a.c = y.npix, y.c
+    a.y, a.ldy = y.ptr, y.ld
+    a.mu, a.ldmu = mu.ptr, mu.ld
+    a.scale, a.ldsc = scale.ptr, scale.ld
+    a.yq, a.ldyq = _ptr(yq)
+    a.yq2, a.ldyq2 = _ptr(yq2)
+    a.symbols, a.ldsym = _ptr(symbols)
+    a.likelihood, a.ldlik = _ptr(likelihood)
+    n = -(-(y.npix * y.c) // 256)
+    if part_off + n > partials.numel():
+        raise ValueError("gauss_rate: partials buffer too small")
+    a.partials = partials.data_ptr() + part_off * 8
+    a.max_parts = partials.numel() - part_off
+    a.scale_bound, a.likelihood_bound = scale_bound, likelihood_bound
+    check(_lib().lic_gauss_rate_fwd(ctypes.byref(a), stream_handle()))
+    return n
+
+
+def bpp_finalize(partials: torch.Tensor, nparts: int, num_pixels: float, out: torch.Tensor,
+                 sum_out: Optional[torch.Tensor] = None):
+    check(_lib().lic_bpp_finalize(partials.data_ptr(), nparts, float(num_pixels), out.data_ptr(),
+                                  sum_out.data_ptr() if sum_out is not None else None, stream_handle()))
+
+
+def syntax_recon(xtil: Act, wgen: Act, x: torch.Tensor, x_rec: torch.Tensor, parts: torch.Tensor,
+                 parts_per_img: int):
+    B, _, H, W = x.shape
+    check(_lib().lic_syntax_recon_fwd(dtype_id(xtil.dtype), xtil.ptr, B, H, W, xtil.c, xtil.ld, wgen.ptr, wgen.ld,
+                                      x.data_ptr(), x_rec.data_ptr(), parts.data_ptr(), parts_per_img,
+                                      stream_handle()))
+
+
+def psnr_finalize(parts: torch.Tensor, B: int, parts_per_img: int, count: float, v_mse: torch.Tensor,
+                  v_psnr: torch.Tensor):
+    check(_lib().lic_psnr_finalize(parts.data_ptr(), B, parts_per_img, float(count), v_mse.data_ptr(),
+                                   v_psnr.data_ptr(), stream_handle()))
+
+
+def to_nchw_f32(x: Act) -> torch.Tensor:
+    out = torch.empty((x.B, x.c, x.H, x.W), dtype=torch.float32, device=x.t.device)
+    check(_lib().lic_nhwc_to_nchw(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.c, x.ld, out.data_ptr(),
+                                  stream_handle()))
+    return out

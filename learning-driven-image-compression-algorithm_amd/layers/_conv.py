@@ -1,0 +1,95 @@
+"""nn.Conv2d / nn.ConvTranspose2d / nn.Linear with the reference's parameter names
+(``weight``, ``bias``) whose compute runs on liblic.
+
+Packed weights ([copad][taps][cpad] in the activation dtype) are cached per
+(dtype, geometry) and rebuilt when a parameter is modified in place (its
+``_version`` changes) or moved.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import functional as Fn
+from .._ffi import ACT_NONE, EPI_PLAIN, PRO_NONE
+from ..functional import Act
+
+
+def _param_key(*ps):
+    return tuple((p.data_ptr(), p._version) if p is not None else None for p in ps)
+
+
+class _PackCache:
+    def _get_pack(self, key, build):
+        cache = self.__dict__.setdefault("_lic_packs", {})
+        ent = cache.get(key)
+        pk = _param_key(self.weight, self.bias)
+        if ent is None or ent[0] != pk:
+            ent = (pk, build())
+            cache[key] = ent
+        return ent[1]
+
+
+class Conv2d(nn.Conv2d, _PackCache):
+    """nn.Conv2d (square kernel, symmetric padding) executed by lic_conv2d_fwd."""
+
+    def packed(self, dtype: torch.dtype, pad: Optional[Tuple[int, int, int, int]] = None) -> Fn.ConvPack:
+        if pad is None:
+            p = self.padding[0]
+            pad = (p, p, p, p)
+        return self._get_pack((dtype, pad), lambda: Fn.pack_conv2d(self.weight, self.bias, self.stride[0], pad,
+                                                                    dtype, self.groups))
+
+    def run(self, x: Act, out: Optional[Act] = None, *, pad=None, act: int = ACT_NONE, slope: float = 0.01,
+            epi: int = EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
+            y2: Optional[Act] = None, prologue: int = PRO_NONE, shuffle: bool = False) -> Act:
+        pk = self.packed(x.dtype, pad)
+        return Fn.conv(x, pk, out, act=act, slope=slope, epi=epi, r1=r1, g=g, r2=r2, y2=y2, prologue=prologue,
+                       shuffle=shuffle)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.run(Act.from_nchw(x)).nchw()
+
+
+class Linear(nn.Linear, _PackCache):
+    """nn.Linear applied per pixel of an NHWC map (a 1x1 convolution)."""
+
+    def packed(self, dtype: torch.dtype) -> Fn.ConvPack:
+        return self._get_pack(dtype, lambda: Fn.pack_conv2d(self.weight[:, :, None, None], self.bias, 1,
+                                                             (0, 0, 0, 0), dtype))
+
+    def run(self, x: Act, out: Optional[Act] = None, **kw) -> Act:
+        return Fn.conv(x, self.packed(x.dtype), out, **kw)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shp = x.shape
+        t = x.reshape(-1, 1, 1, shp[-1]).contiguous()
+        out = self.run(Act(t))
+        return out.t.reshape(*shp[:-1], self.out_features)
+
+
+class ConvTranspose2d(nn.ConvTranspose2d, _PackCache):
+    """nn.ConvTranspose2d as stride^2 sub-pixel phase convolutions (gather form),
+    optionally preceded by ZeroPad2d(left=prepad[1], top=prepad[0])."""
+
+    def packed(self, dtype: torch.dtype, prepad=(0, 0)):
+        return self._get_pack((dtype, prepad), lambda: Fn.pack_conv_transpose2d(
+            self.weight, self.bias, self.stride[0], self.padding[0], self.output_padding[0], dtype, prepad))
+
+    def out_hw(self, H, W, prepad=(0, 0)):
+        return Fn.convT_out_hw(H, W, self.stride[0], self.padding[0], self.output_padding[0], self.kernel_size[0],
+                               prepad)
+
+    def run(self, x: Act, out: Optional[Act] = None, *, prepad=(0, 0), **kw) -> Act:
+        packs = self.packed(x.dtype, prepad)
+        Ho, Wo = self.out_hw(x.H, x.W, prepad)
+        if self.stride[0] == 1 and self.kernel_size[0] == 1 and self.padding[0] == 0:
+            # 1x1 stride-1 transposed conv == 1x1 conv with the transposed weight (one phase).
+            return Fn.conv(x, packs[0], out if out is not None else Act.empty(x.B, Ho, Wo, packs[0].co, x.dtype,
+                                                                               x.t.device), **kw)
+        return Fn.conv_transpose(x, packs, Ho, Wo, out, **kw)
+
+    def forward(self, x: torch.Tensor, output_size=None) -> torch.Tensor:
+        return self.run(Act.from_nchw(x)).nchw()

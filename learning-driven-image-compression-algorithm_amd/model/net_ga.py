@@ -1,0 +1,523 @@
+"""net_ga: the codec graph evaluated by the reference eval_net.py (model/net_ga.py).
+
+Same class names, constructor signatures and state_dict keys as the reference;
+every layer executes on liblic (HIP, gfx950).  ``Net.forward(inputs, mode, num)``
+returns ``(bpp, v_mse, v_psnr)`` for mode='test' and ``(bpp, mse)`` for
+mode='train', like net_ga.py:981-1144, with eval ('dequantize') quantisation
+semantics and without the reference's visualisation / PNG side effects.
+
+Deviations (documented in DESIGN.md):
+  * ``Net.__init__`` does not call ``get_parser().parse_args()`` (net_ga.py:739-740
+    parses the *process* argv and rejects eval_net.py's own flags).
+  * The EntropyBottleneck likelihoods (computed and discarded, net_ga.py:996) and the
+    visual_FeatureMap_heat re-runs (:989-990, :1008-1009) are not executed.
+  * BlockSample / NeighborSample constant buffers (~425 MB, unused in forward) are not
+    materialised; their keys are accepted and ignored by load_state_dict.
+  * post_processing=True (HAN) is not implemented yet (raises).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import functional as Fn
+from .._ffi import ACT_GELU, ACT_LRELU, ACT_RELU, ACT_ROUND, EPI_GATE, EPI_HALF_TANH
+from ..functional import Act
+from ..layers._conv import Conv2d, ConvTranspose2d, Linear
+from ..layers.compressai import (AttentionBlock, EntropyBottleneck, GaussianConditional, ResidualBlockWithStride,
+                                 subpel_conv3x3)
+from ..layers.layers import Win_noShift_Attention
+from .Block_unet import WMSA, ResidualBottleneck
+from .gdn import GDN, IGDN
+
+__all__ = ["Net", "analysisTransformModel", "synthesisTransformModel", "SWAtten", "SwinBlock", "Block_1",
+           "Syntax_Model", "conv_generator", "DepthwiseSeparableConv", "ResidualBottleneck", "weight_init"]
+
+
+def conv1x1(in_ch: int, out_ch: int, stride: int = 1) -> Conv2d:
+    return Conv2d(in_ch, out_ch, kernel_size=1, stride=stride)
+
+
+def conv3x3(in_ch: int, out_ch: int, stride: int = 1) -> Conv2d:
+    return Conv2d(in_ch, out_ch, kernel_size=3, stride=stride, padding=1)
+
+
+def conv(in_channels, out_channels, kernel_size=5, stride=2) -> Conv2d:
+    """net_ga.py:703-710."""
+    return Conv2d(in_channels, out_channels, kernel_size=kernel_size, stride=stride, padding=kernel_size // 2)
+
+
+def weight_init(m):
+    """net_ga.py:723-729: xavier_uniform weights, zero biases for Conv2d / Linear."""
+    if isinstance(m, nn.Linear):
+        nn.init.xavier_uniform_(m.weight)
+        nn.init.constant_(m.bias, 0)
+    elif isinstance(m, nn.Conv2d):
+        nn.init.xavier_uniform_(m.weight)
+        nn.init.constant_(m.bias, 0)
+
+
+# --------------------------------------------------------------------------- Swin / SWAtten (slice loop)
+class Block_1(nn.Module):
+    """net_ga.py:106-128: x + WMSA(LN(x)); x + MLP(LN(x)) (LayerNorm eps 1e-5)."""
+
+    def __init__(self, input_dim, output_dim, head_dim, window_size, drop_path, type='W', input_resolution=None):
+        super().__init__()
+        self.input_dim = input_dim
+        self.output_dim = output_dim
+        assert type in ['W', 'SW']
+        self.type = type
+        self.ln1 = nn.LayerNorm(input_dim)
+        self.msa = WMSA(input_dim, input_dim, head_dim, window_size, self.type)
+        self.drop_path = nn.Identity()
+        self.ln2 = nn.LayerNorm(input_dim)
+        self.mlp = nn.Sequential(Linear(input_dim, 4 * input_dim), nn.GELU(), Linear(4 * input_dim, output_dim))
+
+    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        y = Fn.layernorm(x, self.ln1.weight, self.ln1.bias, self.ln1.eps)
+        x1 = self.msa.run(y, residual=x)
+        y = Fn.layernorm(x1, self.ln2.weight, self.ln2.bias, self.ln2.eps)
+        h = self.mlp[0].run(y, act=ACT_GELU)
+        return self.mlp[2].run(h, out, r1=x1)
+
+
+class SwinBlock(nn.Module):
+    """net_ga.py:131-150 (W block then SW block)."""
+
+    def __init__(self, input_dim, output_dim, head_dim, window_size, drop_path) -> None:
+        super().__init__()
+        self.block_1 = Block_1(input_dim, output_dim, head_dim, window_size, drop_path, type='W')
+        self.block_2 = Block_1(input_dim, output_dim, head_dim, window_size, drop_path, type='SW')
+        self.window_size = window_size
+
+    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        ws = self.window_size
+        if x.W <= ws or x.H <= ws:
+            # reference pads (pc, pc+1, pr, pr+1) and returns the padded map (`resize` stays False)
+            pr, pc = (ws - x.H) // 2, (ws - x.W) // 2
+            t = x.t[..., x.c0:x.c0 + x.c]
+            t = F.pad(t.permute(0, 3, 1, 2), (pc, pc + 1, pr, pr + 1)).permute(0, 2, 3, 1).contiguous()
+            if t.shape[1] % ws or t.shape[2] % ws:
+                raise ValueError("SwinBlock: padded latent is not a multiple of the window (the reference fails "
+                                 "here too: net_ga.py:139-145)")
+            x = Act(t)
+            out = None
+        t = self.block_1.run(x)
+        return self.block_2.run(t, out)
+
+
+class SWAtten(AttentionBlock):
+    """net_ga.py:153-174: in_conv -> [conv_a(x) * sigmoid(conv_b(swin(x))) + x] -> out_conv."""
+
+    def __init__(self, input_dim, output_dim, head_dim, window_size, drop_path, inter_dim=192) -> None:
+        if inter_dim is not None:
+            super().__init__(N=inter_dim)
+            self.non_local_block = SwinBlock(inter_dim, inter_dim, head_dim, window_size, drop_path)
+        else:
+            super().__init__(N=input_dim)
+            self.non_local_block = SwinBlock(input_dim, input_dim, head_dim, window_size, drop_path)
+        if inter_dim is not None:
+            self.in_conv = conv1x1(input_dim, inter_dim)
+            self.out_conv = conv1x1(inter_dim, output_dim)
+
+    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        x = self.in_conv.run(x)
+        z = self.non_local_block.run(x)
+        a = x
+        for u in self.conv_a:
+            a = u.run(a)
+        b = z
+        for u in list(self.conv_b)[:3]:
+            b = u.run(b)
+        g = self.conv_b[3].run(b, epi=EPI_GATE, g=a, r2=x)
+        return self.out_conv.run(g, out)
+
+    def forward(self, x):
+        return self.run(Act.from_nchw(x)).nchw()
+
+
+# --------------------------------------------------------------------------- transforms
+class analysisTransformModel(nn.Module):
+    """Encoder g_a, net_ga.py:253-309."""
+
+    def __init__(self, in_dim, num_filters, conv_trainable=True):
+        super().__init__()
+        self.transform = nn.Sequential(
+            ResidualBottleneck(in_dim), ResidualBottleneck(in_dim), ResidualBottleneck(in_dim),
+            ResidualBlockWithStride(in_dim, num_filters[0], stride=2),
+            GDN(num_filters[0]),
+            nn.ZeroPad2d((1, 2, 1, 2)),
+            Conv2d(num_filters[0], num_filters[1], 5, 2, 0),
+            GDN(num_filters[1]),
+            Win_noShift_Attention(dim=num_filters[1], num_heads=8, window_size=8, shift_size=4),
+            ResidualBottleneck(num_filters[1]), ResidualBottleneck(num_filters[1]), ResidualBottleneck(num_filters[1]),
+            ResidualBlockWithStride(num_filters[1], num_filters[2], 2),
+            GDN(num_filters[2]),
+            nn.ZeroPad2d((1, 2, 1, 2)),
+            Conv2d(num_filters[2], num_filters[3], 5, 2, 0),
+            Win_noShift_Attention(dim=num_filters[3], num_heads=8, window_size=4, shift_size=2),
+        )
+
+    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        t = self.transform
+        for i in range(3):
+            x = t[i].run(x)
+        x = t[3].run(x)
+        x = t[4].run(x)
+        x = t[6].run(x, pad=(1, 1, 2, 2))     # ZeroPad2d((1, 2, 1, 2)) = left 1, right 2, top 1, bottom 2
+        x = t[7].run(x)
+        x = t[8].run(x)
+        for i in (9, 10, 11):
+            x = t[i].run(x)
+        x = t[12].run(x)
+        x = t[13].run(x)
+        x = t[15].run(x, pad=(1, 1, 2, 2))
+        return t[16].run(x, out)
+
+    def forward(self, inputs):
+        return self.run(Act.from_nchw(inputs)).nchw()
+
+
+class synthesisTransformModel(nn.Module):
+    """Decoder g_s, net_ga.py:364-403 (ZeroPad2d((1,0,1,0)) + ConvTranspose2d(5, 2, 3, op=1) + IGDN)."""
+
+    def __init__(self, in_dim, num_filters, conv_trainable=True):
+        super().__init__()
+        self.transform = nn.Sequential(
+            Win_noShift_Attention(dim=in_dim, num_heads=8, window_size=4, shift_size=2),
+            nn.ZeroPad2d((1, 0, 1, 0)),
+            ConvTranspose2d(in_dim, num_filters[0], 5, 2, 3, output_padding=1),
+            IGDN(num_filters[0], inverse=True),
+            nn.ZeroPad2d((1, 0, 1, 0)),
+            ConvTranspose2d(num_filters[0], num_filters[1], 5, 2, 3, output_padding=1),
+            IGDN(num_filters[1], inverse=True),
+            Win_noShift_Attention(dim=num_filters[1], num_heads=8, window_size=8, shift_size=2),
+            nn.ZeroPad2d((1, 0, 1, 0)),
+            ConvTranspose2d(num_filters[1], num_filters[2], 5, 2, 3, output_padding=1),
+            IGDN(num_filters[2], inverse=True),
+            nn.ZeroPad2d((1, 0, 1, 0)),
+            ConvTranspose2d(num_filters[2], num_filters[3], 5, 2, 3, output_padding=1),
+            IGDN(num_filters[3], inverse=True),
+        )
+
+    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        t = self.transform
+        x = t[0].run(x)
+        x = t[2].run(x, prepad=(1, 1))
+        x = t[3].run(x)
+        x = t[5].run(x, prepad=(1, 1))
+        x = t[6].run(x)
+        x = t[7].run(x)
+        x = t[9].run(x, prepad=(1, 1))
+        x = t[10].run(x)
+        x = t[12].run(x, prepad=(1, 1))
+        return t[13].run(x, out)
+
+    def forward(self, inputs):
+        return self.run(Act.from_nchw(inputs)).nchw()
+
+
+def _run_seq_gelu(seq: nn.Sequential, x: Act, out: Optional[Act] = None) -> Act:
+    """conv (GELU conv)* stacks of net_ga.py:811-845; subpel convs fuse PixelShuffle(2)."""
+    mods = list(seq)
+    convs = [m for m in mods if not isinstance(m, nn.GELU)]
+    for k, m in enumerate(convs):
+        last = k == len(convs) - 1
+        kw = dict(act=0 if last else ACT_GELU)
+        if isinstance(m, nn.Sequential):  # subpel_conv3x3 = conv3x3 + PixelShuffle(2)
+            x = m[0].run(x, shuffle=True, **kw)
+        else:
+            x = m.run(x, out if last else None, **kw)
+    return x
+
+
+class DepthwiseSeparableConv(nn.Module):
+    """Restatement of the missing reference model/DepthwiseSeparableConv.py (UNPINNED):
+    depthwise 3x3 (groups=C, pad 1, bias) + pointwise 1x1 (bias)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, padding=1):
+        super().__init__()
+        self.depthwise = Conv2d(in_channels, in_channels, kernel_size, 1, padding, groups=in_channels)
+        self.pointwise = Conv2d(in_channels, out_channels, 1)
+
+    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        return self.pointwise.run(self.depthwise.run(x), out)
+
+
+class conv_generator(nn.Module):
+    """net_ga.py:583-604: MLP 16 -> 128 -> 256 -> 3*out_dim (LeakyReLU 0.2)."""
+
+    def __init__(self, in_dim, out_dim):
+        super().__init__()
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.transform = nn.Sequential(Linear(in_dim, 128), nn.LeakyReLU(0.2), Linear(128, 256), nn.LeakyReLU(0.2),
+                                       Linear(256, out_dim * 3))
+
+    def run(self, x: Act) -> Act:
+        """x: [B, 1, 1, in_dim] view -> [B, 1, 1, 3*out_dim] (row-major (3, out_dim))."""
+        h = self.transform[0].run(x, act=ACT_LRELU, slope=0.2)
+        h = self.transform[2].run(h, act=ACT_LRELU, slope=0.2)
+        return self.transform[4].run(h)
+
+
+class Syntax_Model(nn.Module):
+    """net_ga.py:610-647 (the bypass_round of :1016 is fused into the last conv)."""
+
+    def __init__(self, in_dim, out_dim):
+        super().__init__()
+        self.Depth_down0 = DepthwiseSeparableConv(in_channels=16, out_channels=16)
+        self.down0 = Conv2d(in_dim, 32, 3, 2, 1)
+        self.Depth_down1 = DepthwiseSeparableConv(in_channels=32, out_channels=32)
+        self.down1 = Conv2d(32, 64, 3, 2, 1)
+        self.Depth_down2 = DepthwiseSeparableConv(in_channels=64, out_channels=64)
+        self.down2 = Conv2d(64, 128, 3, 2, 1)
+        self.WAM = Win_noShift_Attention(dim=64, num_heads=8, window_size=4, shift_size=2)
+        self.conv = Conv2d(in_dim + 32 + 64 + 128, out_dim, 1, 1, 0)
+        self.pooling = nn.AdaptiveAvgPool2d(1)
+
+    def run(self, s: Act, rounded: bool = True) -> Act:
+        B = s.B
+        pooled = Act.empty(B, 1, 1, s.c + 32 + 64 + 128, s.dtype, s.t.device)
+        Fn.avgpool(s, pooled.ch(0, s.c))
+        ds1 = self.down0.run(self.Depth_down0.run(s), act=ACT_RELU)
+        Fn.avgpool(ds1, pooled.ch(s.c, s.c + 32))
+        ds2 = self.down1.run(self.Depth_down1.run(ds1), act=ACT_RELU)
+        ds2 = self.WAM.run(ds2)
+        Fn.avgpool(ds2, pooled.ch(s.c + 32, s.c + 96))
+        ds3 = self.down2.run(self.Depth_down2.run(ds2), act=ACT_RELU)
+        Fn.avgpool(ds3, pooled.ch(s.c + 96, s.c + 224))
+        return self.conv.run(pooled, act=ACT_ROUND if rounded else 0)
+
+    def forward(self, syntax):
+        return self.run(Act.from_nchw(syntax), rounded=False).nchw()
+
+
+class PredictionModel_Context(nn.Module):
+    """net_ga.py:548-580 — parameters only (not on the Net.forward path)."""
+
+    def __init__(self, in_dim, dim=192, trainable=True, outdim=None):
+        super().__init__()
+        outdim = dim if outdim is None else outdim
+        self.transform = nn.Sequential(Conv2d(in_dim, dim, 3, 1, 1), nn.LeakyReLU(0.2), Conv2d(dim, dim, 3, 2, 1),
+                                       nn.LeakyReLU(0.2), Conv2d(dim, dim, 3, 1, 1), nn.LeakyReLU(0.2))
+        self.fc = Linear(dim * 2 * 2, outdim)
+        self.flatten = nn.Flatten()
+
+
+class PredictionModel_Syntax(nn.Module):
+    """net_ga.py:650-687 — parameters only (not on the Net.forward path)."""
+
+    def __init__(self, in_dim, dim=192, trainable=True, outdim=None):
+        super().__init__()
+        outdim = dim if outdim is None else outdim
+        self.down0 = Conv2d(in_dim, dim, 3, 2, 1)
+        self.down1 = Conv2d(dim, dim, 3, 2, 1)
+        self.pooling = nn.AdaptiveAvgPool2d(1)
+        self.WAM = Win_noShift_Attention(dim=dim, num_heads=8, window_size=4, shift_size=2)
+        self.fc = Linear(dim * 2 + in_dim, outdim)
+        self.flatten = nn.Flatten()
+
+
+class _Stateless(nn.Module):
+    """Placeholder for reference modules without parameters/buffers that are not on the
+    forward path (GaussianModel, NoiseQuant)."""
+
+
+_IGNORED_PREFIXES = ("y_sampler.", "h_sampler.", "test_y_sampler.", "test_h_sampler.", "HAN.",
+                     "conv_weights_gen_HAN.", "add_mean.")
+
+
+class Net(nn.Module):
+    """net_ga.Net (net_ga.py:735-1144).  ``precision`` selects the activation dtype of
+    the HIP path: 'fp32' (parity) or 'fp16' (fp32 accumulation)."""
+
+    arch = "net_ga"
+
+    def __init__(self, train_size, test_size, is_high, post_processing, precision: str = "fp32"):
+        super().__init__()
+        self.mse = nn.MSELoss()
+        self.num_slices = 4
+        self.max_support_slices = 4
+        self.gaussian_conditional = GaussianConditional(None)
+        self.train_size = train_size
+        self.test_size = test_size
+        self.post_processing = post_processing
+        self.is_high = is_high
+        self.precision = precision
+        N, M = (384, 32) if is_high else (192, 16)
+        self.M, self.N = M, N
+        self.conv_1 = conv1x1(192, 4)
+        self.conv_2 = conv1x1(4, 192)
+        self.a_model = analysisTransformModel(3, [N, N, N, N])
+        self.a_model.apply(weight_init)
+        self.s_model = synthesisTransformModel(N, [N, N, N, M])
+        self.s_model.apply(weight_init)
+        self.syntax_model = Syntax_Model(M, M)
+        self.syntax_model.apply(weight_init)
+        self.conv_weights_gen = conv_generator(in_dim=M, out_dim=M)
+        self.conv_weights_gen.apply(weight_init)
+        self.quant_noise = _Stateless()
+        self._build_hyper()
+        self.entropy_bottleneck_z2 = _Stateless()
+        self.entropy_bottleneck_z3 = _Stateless()
+        self.entropy_bottleneck = EntropyBottleneck(self._eb_channels)
+        self.entropy_bottleneck_z3_syntax = _Stateless()
+        self.window_size = 8
+        ns = self.num_slices
+        cin = lambda i: 192 + (192 // ns) * min(i, 4)
+        self.atten_mean = nn.ModuleList(nn.Sequential(SWAtten(cin(i), cin(i), 16, self.window_size, 0, inter_dim=128))
+                                        for i in range(ns))
+        self.cc_mean_transforms = nn.ModuleList(
+            nn.Sequential(conv(cin(i), 224, stride=1, kernel_size=3), nn.GELU(), conv(224, 128, stride=1, kernel_size=3),
+                          nn.GELU(), conv(128, 192 // ns, stride=1, kernel_size=3)) for i in range(ns))
+        self.cc_mean_transforms.apply(weight_init)
+        self.atten_scale = nn.ModuleList(nn.Sequential(SWAtten(cin(i), cin(i), 16, self.window_size, 0, inter_dim=128))
+                                         for i in range(ns))
+        self.cc_scale_transforms = nn.ModuleList(
+            nn.Sequential(conv(cin(i), 224, stride=1, kernel_size=3), nn.GELU(), conv(224, 128, stride=1, kernel_size=3),
+                          nn.GELU(), conv(128, 192 // ns, stride=1, kernel_size=3)) for i in range(ns))
+        self.cc_scale_transforms.apply(weight_init)
+        self.lrp_transforms = nn.ModuleList(
+            nn.Sequential(conv(192 + (192 // ns) * min(i + 1, 5), 224, stride=1, kernel_size=3), nn.GELU(),
+                          conv(224, 128, stride=1, kernel_size=3), nn.GELU(),
+                          conv(128, 192 // ns, stride=1, kernel_size=3)) for i in range(ns))
+        self.v_z2_sigma = nn.Parameter(torch.ones((1, N, 1, 1), dtype=torch.float32, requires_grad=True))
+        self.register_parameter('z2_sigma', self.v_z2_sigma)
+        self.prediction_model = PredictionModel_Context(in_dim=2 * N - M, dim=N, outdim=(N - M) * 2)
+        self.prediction_model.apply(weight_init)
+        self.prediction_model_syntax = PredictionModel_Syntax(in_dim=N, dim=M, outdim=M * 2)
+        self.prediction_model_syntax.apply(weight_init)
+        self.last: Dict[str, torch.Tensor] = {}
+
+    # ---- hyper prior (overridden by net_unet_ha_hs)
+    _eb_channels = 192
+
+    def _build_hyper(self):
+        self.h_a = nn.Sequential(conv3x3(192, 320), nn.GELU(), conv3x3(320, 288), nn.GELU(),
+                                 conv3x3(288, 256, stride=2), nn.GELU(), conv3x3(256, 224), nn.GELU(),
+                                 conv3x3(224, 192, stride=2))
+        mk = lambda: nn.Sequential(conv3x3(192, 192), nn.GELU(), subpel_conv3x3(192, 224, 2), nn.GELU(),
+                                   conv3x3(224, 256), nn.GELU(), subpel_conv3x3(256, 288, 2), nn.GELU(),
+                                   conv3x3(288, 192))
+        self.h_mean_s = mk()
+        self.h_scale_s = mk()
+
+    def _hyper(self, z3: Act, means_out: Act, scales_out: Act):
+        """net_ga.py:993-1007: z = h_a(y); z_hat = round(z - m) + m; scales/means = h_*_s(z_hat)."""
+        z = _run_seq_gelu(self.h_a, z3)
+        z_hat = Fn.quantize_median(z, self.entropy_bottleneck.medians_flat().to(z.t.device))
+        _run_seq_gelu(self.h_scale_s, z_hat, scales_out)
+        _run_seq_gelu(self.h_mean_s, z_hat, means_out)
+        return z, z_hat
+
+    _shared_support = False  # net_unet_ha_hs: latent_scales == latent_means
+
+    # ---- state dict compatibility
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        sd = {k: v for k, v in state_dict.items() if not k.startswith(_IGNORED_PREFIXES)}
+        return super().load_state_dict(sd, strict=strict, assign=assign)
+
+    def base_params(self):
+        params = []
+        params += self.a_model.parameters()
+        params += self.s_model.parameters()
+        params += self.h_a.parameters()
+        for m in self._hyper_s_modules():
+            params += m.parameters()
+        params += self.syntax_model.parameters()
+        params += self.conv_weights_gen.parameters()
+        params += self.prediction_model.parameters()
+        params += self.prediction_model_syntax.parameters()
+        params.append(self.v_z2_sigma)
+        return params
+
+    def _hyper_s_modules(self):
+        return [self.h_scale_s, self.h_mean_s]
+
+    @property
+    def dtype(self):
+        return torch.float16 if self.precision == "fp16" else torch.float32
+
+    # ---- forward
+    @torch.no_grad()
+    def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False):
+        if self.post_processing:
+            raise NotImplementedError("post_processing (HAN) is not implemented on the HIP path yet")
+        if not inputs.is_cuda:
+            raise RuntimeError("lic_amd Net runs on the GPU only (HIP path); move inputs to cuda")
+        if mode != 'test':
+            raise NotImplementedError("mode='train' needs the backward kernels (SURVEY.md 8(f) rank 1); "
+                                      "use mode='test'")
+        b, h, w, c = self.train_size
+        x_in = inputs.contiguous().float()
+        B, _, H, W = x_in.shape
+        dev, dt = x_in.device, self.dtype
+        x = Act.from_nchw(x_in, dt)
+        z3 = self.a_model.run(x)                                  # net_ga.py:988
+        hh, ww = z3.H, z3.W
+        ns, sw = self.num_slices, 192 // self.num_slices
+        # concat buffers: MS = [latent_means | y_hat_0..3], SS = [latent_scales | y_hat_0..2]
+        MS = Act.empty(B, hh, ww, 192 + 192, dt, dev)
+        SS = MS if self._shared_support else Act.empty(B, hh, ww, 192 + 144, dt, dev)
+        z, z_hat = self._hyper(z3, MS.ch(0, 192), SS.ch(0, 192))
+        syn_r = self.syntax_model.run(z3.ch(0, self.M))            # net_ga.py:1010-1016
+        LR = Act.empty(B, hh, ww, 192 + sw * 4, dt, dev)           # lrp_support (widest: 384)
+        MU = Act.empty(B, hh, ww, 192, dt, dev)
+        SC = Act.empty(B, hh, ww, 192, dt, dev)
+        SYM = torch.empty((B, hh, ww, 192), dtype=torch.int32, device=dev)
+        LIK = torch.empty((B, hh, ww, 192), dtype=torch.float32, device=dev) if return_intermediates else None
+        nper = -(-(B * hh * ww * sw) // 256)
+        partials = torch.empty((ns * nper,), dtype=torch.float64, device=dev)
+        for i in range(ns):                                        # net_ga.py:1028-1062
+            ci = 192 + sw * min(i, 4)
+            ms = self.atten_mean[i][0].run(MS.ch(0, ci), out=LR.ch(0, ci))
+            cm = self.cc_mean_transforms[i]
+            t = cm[0].run(ms, act=ACT_GELU)
+            t = cm[2].run(t, act=ACT_GELU)
+            mu = cm[4].run(t, out=MU.ch(sw * i, sw * (i + 1)))
+            ss = self.atten_scale[i][0].run(SS.ch(0, ci))
+            cs = self.cc_scale_transforms[i]
+            t = cs[0].run(ss, act=ACT_GELU)
+            t = cs[2].run(t, act=ACT_GELU)
+            sc = cs[4].run(t, out=SC.ch(sw * i, sw * (i + 1)))
+            yq = LR.ch(ci, ci + sw)
+            Fn.gauss_rate(z3.ch(sw * i, sw * (i + 1)), mu, sc, partials, i * nper, yq=yq,
+                          symbols=Act(SYM, sw * i, sw),
+                          likelihood=Act(LIK, sw * i, sw) if LIK is not None else None,
+                          scale_bound=self.gaussian_conditional._scale_bound,
+                          likelihood_bound=self.gaussian_conditional._likelihood_bound)
+            lr = self.lrp_transforms[i]
+            t = lr[0].run(LR.ch(0, ci + sw), act=ACT_GELU)
+            t = lr[2].run(t, act=ACT_GELU)
+            y2 = SS.ch(192 + sw * i, 192 + sw * (i + 1)) if (not self._shared_support and i < ns - 1) else None
+            lr[4].run(t, out=MS.ch(192 + sw * i, 192 + sw * (i + 1)), epi=EPI_HALF_TANH, r2=yq, y2=y2)
+        y_hat = MS.ch(192, 384)
+        x_tilde = self.s_model.run(y_hat)                          # net_ga.py:1078
+        cw = self.conv_weights_gen.run(syn_r)                      # net_ga.py:1083
+        x_rec = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
+        ppi = max(1, min(64, -(-(H * W) // 4096)))
+        sq_parts = torch.empty((B * ppi,), dtype=torch.float64, device=dev)
+        Fn.syntax_recon(x_tilde, cw, x_in, x_rec, sq_parts, ppi)   # :1089-1092, :1118, :1137-1141
+        num_pixels = B * h * w
+        bpp = torch.empty((1,), dtype=torch.float32, device=dev)
+        Fn.bpp_finalize(partials, ns * nper, num_pixels, bpp)      # :1134
+        v_mse = torch.empty((B,), dtype=torch.float32, device=dev)
+        v_psnr = torch.empty((1,), dtype=torch.float32, device=dev)
+        Fn.psnr_finalize(sq_parts, B, ppi, 3.0 * H * W, v_mse, v_psnr)
+        if return_intermediates:
+            self.last = dict(z3=z3.nchw(), z=z.nchw(), z_hat=z_hat.nchw(), latent_means=MS.ch(0, 192).nchw(),
+                             latent_scales=SS.ch(0, 192).nchw(), y_hat=y_hat.nchw(), means=MU.nchw(),
+                             scales=SC.nchw(), symbols=SYM.permute(0, 3, 1, 2), likelihoods=LIK.permute(0, 3, 1, 2),
+                             x_tilde=x_tilde.nchw(), x_rec=x_rec, syntax=syn_r.nchw())
+        return bpp[0], v_mse, v_psnr[0]

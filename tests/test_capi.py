@@ -1,0 +1,42 @@
+"""The C-ABI library loads (no GPU needed) and exports every symbol include/lic.h declares."""
+import pathlib
+import re
+
+import lic_amd
+from lic_amd import _ffi
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def _declared():
+    txt = (ROOT / "include" / "lic.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(lic_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    decl = _declared()
+    assert set(decl) == set(_ffi.EXPORTED_SYMBOLS), (set(decl) ^ set(_ffi.EXPORTED_SYMBOLS))
+
+
+def test_library_exports_all_declared_symbols():
+    assert _ffi.LIB_PATH.exists(), "liblic.so not built (run __graft_entry__.build())"
+    present = _ffi.symbols_present()
+    missing = [s for s in _declared() if s not in present]
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_version():
+    lib = lic_amd.load_library()
+    assert b"gfx950" in lib.lic_version()
+
+
+def test_ctypes_struct_layout_matches_header():
+    import ctypes
+    # the largest args struct: sizes must agree with the C compiler's layout
+    a = _ffi.ConvArgs()
+    assert ctypes.sizeof(a) % 8 == 0
+    names = [f[0] for f in _ffi.ConvArgs._fields_]
+    hdr = (ROOT / "include" / "lic.h").read_text()
+    body = hdr[hdr.index("typedef struct lic_conv_args"):hdr.index("} lic_conv_args;")]
+    for n in names:
+        assert re.search(r"\b%s\b" % n, body), n

@@ -1,0 +1,147 @@
+"""Known-answer tests pinning the CPU oracle (oracle/ref_cpu.py).  The reference
+ships no tests, fixtures or checkpoints and cannot be run here,
+so these analytic identities are the oracle's pin."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_cpu as R
+
+
+def _gdn_params(C, pfx, gamma_scale=0.1, seed=0, compressai=False):
+    g = torch.Generator().manual_seed(seed)
+    P = {}
+    ped = torch.Tensor([(2 ** -18) ** 2])
+    if compressai:
+        P[pfx + ".beta"] = R.nnp_init(torch.ones(C) + 0.5 * torch.rand(C, generator=g), ped)
+        P[pfx + ".gamma"] = R.nnp_init(gamma_scale * torch.eye(C) + 0.01 * torch.rand(C, C, generator=g), ped)
+        P[pfx + ".beta_reparam.pedestal"] = ped
+        P[pfx + ".gamma_reparam.pedestal"] = ped
+        P[pfx + ".beta_reparam.lower_bound.bound"] = torch.Tensor([(1e-6 + (2 ** -18) ** 2) ** 0.5])
+        P[pfx + ".gamma_reparam.lower_bound.bound"] = torch.Tensor([(0 + (2 ** -18) ** 2) ** 0.5])
+    else:
+        ro = torch.FloatTensor([2 ** -18])
+        P[pfx + ".reparam_offset"] = ro
+        P[pfx + ".pedestal"] = ro ** 2
+        P[pfx + ".beta"] = torch.sqrt(torch.ones(C) + 0.5 * torch.rand(C, generator=g) + ro ** 2)
+        P[pfx + ".gamma"] = torch.sqrt(gamma_scale * torch.eye(C) + 0.01 * torch.rand(C, C, generator=g) + ro ** 2)
+    return P
+
+
+def test_nnp_roundtrip():
+    """ops/parametrizers.py:52-58: init -> forward returns 0.1*I."""
+    ped = torch.Tensor([(2 ** -18) ** 2])
+    bound = torch.Tensor([(0 + (2 ** -18) ** 2) ** 0.5])
+    g = R.nnp_init(0.1 * torch.eye(5), ped)
+    out = R.nnp_forward(g, bound, ped)
+    torch.testing.assert_close(out, 0.1 * torch.eye(5), rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("variant", ["model", "compressai"])
+def test_gdn_gamma_zero(variant):
+    """GDN with Gamma' = 0 returns x / sqrt(beta')."""
+    C = 6
+    x = torch.randn(2, C, 5, 5)
+    P = _gdn_params(C, "g", compressai=variant == "compressai")
+    P["g.gamma"] = torch.zeros(C, C)  # clamps to the lower bound -> gamma' = bound^2 - pedestal ~ 0
+    if variant == "compressai":
+        beta = R.nnp_forward(P["g.beta"], P["g.beta_reparam.lower_bound.bound"], P["g.beta_reparam.pedestal"])
+        out = R.gdn_compressai(x, P, "g")
+    else:
+        ped, bb, gb = R.gdn_model_bounds(P, "g")
+        beta = torch.max(P["g.beta"], bb) ** 2 - ped
+        out = R.gdn_model(x, P, "g")
+    ref = x / torch.sqrt(beta).view(1, C, 1, 1)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_igdn_is_x_times_sqrt_norm():
+    C = 4
+    x = torch.randn(1, C, 3, 3)
+    P = _gdn_params(C, "g")
+    ped, bb, gb = R.gdn_model_bounds(P, "g")
+    beta = torch.max(P["g.beta"], bb) ** 2 - ped
+    gamma = torch.max(P["g.gamma"], gb) ** 2 - ped
+    norm = torch.einsum("oi,bihw->bohw", gamma, x ** 2) + beta.view(1, C, 1, 1)
+    torch.testing.assert_close(R.gdn_model(x, P, "g", inverse=True), x * torch.sqrt(norm), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(R.gdn_model(x, P, "g"), x / torch.sqrt(norm), rtol=1e-5, atol=1e-6)
+
+
+def _wba_params(C, heads, ws, pfx, zero=False, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    mk = (lambda *s: torch.zeros(*s)) if zero else (lambda *s: 0.2 * torch.randn(*s, generator=g))
+    return {pfx + ".attn.relative_position_bias_table": mk((2 * ws - 1) ** 2, heads),
+            pfx + ".attn.qkv.weight": mk(3 * C, C), pfx + ".attn.qkv.bias": mk(3 * C),
+            pfx + ".attn.proj.weight": mk(C, C), pfx + ".attn.proj.bias": mk(C)}
+
+
+def test_wba_zero_weights_is_identity():
+    x = torch.randn(2, 16, 8, 8)
+    P = _wba_params(16, 4, 4, "w", zero=True)
+    torch.testing.assert_close(R.win_based_attention(x, P, "w", 4, 4, 2), x)
+
+
+def test_window_partition_bijection():
+    x = torch.randn(2, 16, 8, 3)
+    w = R.window_partition(x, 4)
+    assert w.shape == (2 * 4 * 2, 4, 4, 3)
+    torch.testing.assert_close(R.window_reverse(w, 4, 16, 8), x)
+
+
+def test_wba_mask_full_window_when_ws_equals_h():
+    """With ws == H == W a single window holds all tokens; regions split at H - shift."""
+    m = R.wba_mask(4, 4, 4, 2)
+    assert m.shape == (1, 16, 16)
+    lab = torch.tensor([[0 if y < 2 else 1 for y in range(4)]]).T * 3 + torch.tensor([[0 if x < 2 else 1 for x in range(4)]])
+    lab = lab.reshape(-1)
+    expect = torch.where(lab[None, :] != lab[:, None], -100.0, 0.0)
+    torch.testing.assert_close(m[0], expect)
+
+
+def test_wba_equivariant_to_window_permutation_without_shift():
+    """Without shift, attention is per-window: permuting whole windows commutes with WBA."""
+    torch.manual_seed(0)
+    x = torch.randn(1, 8, 8, 8)
+    P = _wba_params(8, 2, 4, "w")
+    y = R.win_based_attention(x, P, "w", 2, 4, 0)
+    xs = torch.cat([x[:, :, 4:], x[:, :, :4]], dim=2)
+    ys = R.win_based_attention(xs, P, "w", 2, 4, 0)
+    torch.testing.assert_close(torch.cat([ys[:, :, 4:], ys[:, :, :4]], 2), y, rtol=1e-5, atol=1e-6)
+
+
+def test_gaussian_likelihood_integrates_to_one():
+    """Sum over integer bins of the unit-bin likelihood is 1 (means/scale fixed)."""
+    mu, s = torch.tensor([0.3]), torch.tensor([1.7])
+    k = torch.arange(-60, 61, dtype=torch.float32)
+    L = R.gaussian_likelihood(k + 0.0 * mu, s.expand_as(k), mu.expand_as(k))
+    assert abs(L.sum().item() - 1.0) < 1e-5
+    assert torch.all(L >= 1e-9)
+
+
+def test_likelihood_scale_bound_and_floor():
+    L = R.gaussian_likelihood(torch.tensor([0.0, 40.0]), torch.tensor([1e-3, 1e-3]), torch.tensor([0.0, 0.0]))
+    # scale clamps to 0.11: P(|v|<=0.5) at s=0.11 is ~1; far tail clamps to 1e-9
+    assert abs(L[0].item() - (1 - math.erfc(0.5 / 0.11 / math.sqrt(2)))) < 1e-6
+    assert abs(L[1].item() - 1e-9) < 1e-15
+
+
+def test_round_half_even():
+    y = torch.tensor([0.5, 1.5, 2.5, -0.5, -1.5, 2.4999999])
+    assert R.symbols(y, torch.zeros_like(y)).tolist() == [0, 2, 2, 0, -2, 2]
+
+
+def test_ste_round_forward_is_round():
+    x = torch.randn(10000) * 10
+    assert torch.equal(R.ste_round(x), torch.round(x))
+
+
+def test_batch_conv_is_per_image_1x1():
+    torch.manual_seed(0)
+    w = torch.randn(3, 3, 16, 1, 1)
+    x = torch.randn(3, 16, 5, 5)
+    out = R.batch_conv(w, x)
+    ref = torch.einsum("boc,bchw->bohw", w[..., 0, 0], x)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
