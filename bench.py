@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Benchmark: images/s of the full net_ga encode -> quantize -> decode forward
+(eval_net.py's model, Net.forward(x, 'test')) on 256x256 images, batch 32 per GPU
+(BASELINE.json metric + configs[1] batch/size), one process per GPU, images
+sharded across ranks as independent batches (no data-path collective).
+
+One step = one Net.forward over one resident batch (a hipGraph replay of the
+whole forward: a_model, hyper nets, 4-slice entropy loop with on-device rate,
+s_model, syntax head, metrics).  Prints ONE JSON line on rank 0.
+
+Extra fields: roofline (dominant kernel: the 3x3 192->192 MFMA convolution of
+Win_noShift_Attention at 64x64, timed with HIP events on its launch stream),
+a_model (analysis-stack fraction of the fp16 MFMA peak), cpu_baseline (the
+oracle restatement on this host's cores, bounded sample), parity (bpp / PSNR /
+symbols of this run's precision vs the CPU oracle on one image), fp32 (the
+parity-precision path's throughput).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP16_PEAK_TFLOPS = 2516.6   # 256 CU x 4096 FLOP/clk x 2.4 GHz (dense, MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3
+A_MODEL_GFLOP_256 = 85.87   # BASELINE.md / SURVEY.md 8(d): analysis transform per 256x256 image
+FULL_GFLOP_256 = 169.6      # full net forward per 256x256 image
+
+
+def _env_int(k, d):
+    try:
+        return int(os.environ.get(k, d))
+    except ValueError:
+        return d
+
+
+def build_net(arch, precision, size, batch, device, seed=0):
+    from lic_amd.model import net_ga, net_unet_ha_hs
+    torch.manual_seed(seed)
+    mod = net_ga if arch == "net_ga" else net_unet_ha_hs
+    net = mod.Net((batch, size, size, 3), (batch, size, size, 3), False, False, precision=precision)
+    return net
+
+
+def capture(fn, warm=2):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(warm):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = fn()
+    return g, out
+
+
+def time_graph(g, iters):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def dominant_kernel_roofline(dtype, batch, device, iters=30):
+    """conv3x3 192->192 s1 at 64x64 (Win_noShift_Attention @ H/4 of a 256 image): avg launch
+    duration from HIP events recorded on the launch stream."""
+    from lic_amd.layers import Conv2d
+    from lic_amd.functional import Act
+    torch.manual_seed(1)
+    m = Conv2d(192, 192, 3, 1, 1).to(device)
+    x = Act(torch.randn(batch, 64, 64, 192, device=device).to(dtype))
+    out = Act.empty(batch, 64, 64, 192, dtype, device)
+    for _ in range(3):
+        m.run(x, out)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        m.run(x, out)
+    e1.record(st)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    flops = 2.0 * batch * 64 * 64 * 192 * 192 * 9
+    return flops, t
+
+
+def cpu_baseline(arch, size, n_img=2, reps=3):
+    from oracle import ref_cpu as R
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = min(threads, _env_int("OMP_NUM_THREADS", threads))
+    torch.set_num_threads(threads)
+    net = build_net(arch, "fp32", size, n_img, "cpu")
+    P = {k: v.detach().float() for k, v in net.state_dict().items()}
+    x = torch.rand(n_img, 3, size, size, generator=torch.Generator().manual_seed(7)) * 2 - 1
+    R.net_forward(x, P, arch=arch)  # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        R.net_forward(x, P, arch=arch)
+        ts.append(time.perf_counter() - t0)
+    t = statistics.median(ts)
+    return {"value": round(n_img / t, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n_img} x {size}x{size} {arch} encode+decode, oracle/ref_cpu.py (fp32 torch CPU, "
+                      f"reference op order), median of {reps} after 1 warm-up"}
+
+
+def parity_check(arch, precision, size, device):
+    from oracle import ref_cpu as R
+    net = build_net(arch, precision, size, 1, "cpu", seed=3)
+    P = {k: v.detach().float() for k, v in net.state_dict().items()}
+    net = net.to(device)
+    x = torch.rand(1, 3, size, size, generator=torch.Generator().manual_seed(11)) * 2 - 1
+    bpp, v_mse, v_psnr = net(x.to(device), "test", return_intermediates=True)
+    ref = R.net_forward(x, P, arch=arch)
+    mism = (net.last["symbols"].cpu() != ref["symbols"]).float().mean().item()
+    return {"bpp": round(bpp.item(), 7), "bpp_ref": round(ref["bpp"].item(), 7),
+            "d_bpp": abs(bpp.item() - ref["bpp"].item()), "d_psnr_db": abs(v_psnr.item() - ref["v_psnr"].item()),
+            "symbol_mismatch_frac": mism}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--arch", default="net_ga", choices=["net_ga", "net_unet_ha_hs"])
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--no-extras", action="store_true", help="skip cpu baseline / parity / fp32 legs")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = _env_int("WORLD_SIZE", 1)
+    rank = _env_int("RANK", 0)
+    local = _env_int("LOCAL_RANK", 0)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dtype = torch.float16 if args.precision == "fp16" else torch.float32
+
+    net = build_net(args.arch, args.precision, args.size, args.batch, "cpu", seed=0).to(device)
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    x = (torch.rand(args.batch, 3, args.size, args.size, generator=g) * 2 - 1).to(device)
+
+    def step():
+        return net(x, "test")
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    if args.no_graph:
+        run = step
+    else:
+        graph, _ = capture(step)
+        run = graph.replay
+    torch.cuda.synchronize()
+
+    def timed(k):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    elapsed = timed(args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    images = args.batch * args.steps * world
+    value = images / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    result = None
+    if rank == 0:
+        flops, tk = dominant_kernel_roofline(dtype, args.batch, device)
+        peak = FP16_PEAK_TFLOPS if dtype == torch.float16 else FP32_PEAK_TFLOPS
+        achieved = flops / tk / 1e12
+        # analysis transform alone (the north-star roofline target)
+        xa = x.to(dtype).contiguous(memory_format=torch.channels_last)
+        from lic_amd.functional import Act
+        xin = Act(xa.permute(0, 2, 3, 1))
+        ga, _ = capture(lambda: net.a_model.run(xin))
+        ta = time_graph(ga, 10)
+        a_tflops = A_MODEL_GFLOP_256 * (args.size / 256) ** 2 * args.batch / ta / 1e3
+        result = {
+            "metric": "images/sec encode+decode (256x256)",
+            "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "f16" if dtype == torch.float16 else "f32",
+            "data": "synthetic (seeded uniform [-1,1) images, seeded reference-init weights; no checkpoints exist)",
+            "config": {"workload": f"{args.arch} Net.forward(x,'test') encode->quantize->decode, "
+                                   f"{args.size}x{args.size}, batch {args.batch} per GPU, hipGraph replay",
+                       "global_batch": args.batch * world, "image_size": args.size,
+                       "parallelism": f"image-sharded x{world} (independent batches, no collective)"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} (conv_mfma_kernel 128x192), "
+                                   f"{flops / 1e9:.1f} GFLOP/launch, {tk * 1e6:.1f} us/launch"},
+            "a_model": {"ms": round(ta * 1e3, 3), "tflops": round(a_tflops, 2),
+                        "frac_of_peak": round(a_tflops / peak, 4),
+                        "gflop_per_image": A_MODEL_GFLOP_256 * (args.size / 256) ** 2},
+            "full_forward_tflops": round(FULL_GFLOP_256 * (args.size / 256) ** 2 * value / world / 1e3, 2),
+        }
+        if world == 1 and not args.no_extras:
+            result["cpu_baseline"] = cpu_baseline(args.arch, args.size)
+            result["parity"] = parity_check(args.arch, args.precision, args.size, device)
+            if args.precision == "fp16":
+                net32 = build_net(args.arch, "fp32", args.size, args.batch, "cpu", seed=0).to(device)
+                for _ in range(2):
+                    net32(x, "test")
+                g32, _ = capture(lambda: net32(x, "test"))
+                t32 = time_graph(g32, 5)
+                result["fp32"] = {"value": round(args.batch / t32, 2), "unit": "images/s",
+                                  "ms_per_step": round(t32 * 1e3, 3),
+                                  "parity": parity_check(args.arch, "fp32", args.size, device)}
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

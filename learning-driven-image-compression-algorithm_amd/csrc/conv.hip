@@ -19,7 +19,7 @@
 
 namespace lic {
 
-template <typename T, int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, int WM, int WN, int PRO>
 __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_args a, const int M) {
   constexpr int NT = WM * WN * 64;
   constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-B chunk
@@ -116,10 +116,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
       if (A_CH % NT == 0 || q < A_CH) {
         const int row = q >> 2;
         u32x4 v = ra[r];
-        if (a.prologue != LIC_PRO_NONE) {
+        if constexpr (PRO == LIC_PRO_SQUARE) {
           T* e = (T*)&v;
 #pragma unroll
-          for (int k = 0; k < EPC; ++k) e[k] = from_f<T>(apply_pro(to_f(e[k]), a.prologue));
+          for (int k = 0; k < EPC; ++k) {
+            const float f = to_f(e[k]);
+            e[k] = from_f<T>(f * f);
+          }
         }
         *(u32x4*)(base + row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4)) = v;
       }
@@ -192,42 +195,63 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
     }
   }
 
-  // epilogue: lane holds D[row=(r&3)+8(r>>2)+4*half][col=lane&31] per 32x32 tile
+  // Epilogue.  Each wave stages one 32x32 accumulator tile at a time through its
+  // own LDS slot (the accumulator is only indexed with compile-time constants),
+  // then lane l finishes row l>>1, channels (l&1)*16 .. +15 of that tile: bias,
+  // activation, residual / gate / GDN / half-tanh, channel-offset + shuffle
+  // addressing, contiguous stores.
+  float* ct = (float*)smem + wave * (32 * 33);
+  const int erow = lane >> 1, ecol = (lane & 1) * 16;
   T* __restrict__ yg = (T*)a.y;
   T* __restrict__ y2g = (T*)a.y2;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lhalf;
-      const int base = rowpix[row];
-      if (base < 0) continue;
+    for (int j = 0; j < TN; ++j) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WTN + j * 32 + lrow;
-        if (n >= a.co) continue;
-        int64_t pix = base;
-        int ch = n;
-        if (a.out_shuffle == 2) {
-          pix += ((n >> 1) & 1) * a.wo + (n & 1);
-          ch = n >> 2;
+      for (int r = 0; r < 16; ++r) ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[i][j][r];
+      __syncthreads();
+      const int base = rowpix[wm * WTM + i * 32 + erow];
+      const int nb = n0 + wn * WTN + j * 32 + ecol;
+      if (base >= 0) {
+        for (int c = 0; c < 16; ++c) {
+          const int n = nb + c;
+          if (n >= a.co) break;
+          int64_t pix = base;
+          int ch = n;
+          if (a.out_shuffle == 2) {
+            pix += ((n >> 1) & 1) * a.wo + (n & 1);
+            ch = n >> 2;
+          }
+          const float v = conv_epilogue<T>(a, ct[erow * 33 + ecol + c], n, pix, ch);
+          yg[pix * a.ldy + ch] = from_f<T>(v);
+          if (y2g) y2g[pix * a.ldy2 + ch] = from_f<T>(v);
         }
-        const float v = conv_epilogue<T>(a, acc[i][j][r], n, pix, ch);
-        yg[pix * a.ldy + ch] = from_f<T>(v);
-        if (y2g) y2g[pix * a.ldy2 + ch] = from_f<T>(v);
       }
+      __syncthreads();
     }
   }
 }
 
-// Direct (VALU) convolution: one thread per (output pixel, output channel).
-// Used for tiny / misaligned channel counts (Cin = 1, 3, grouped/depthwise).
-template <typename T>
-__global__ __launch_bounds__(256) void conv_direct_kernel(const lic_conv_args a, const int64_t M) {
+// Direct (VALU) convolution for tiny / misaligned channel counts (Cin = 1 or 3,
+// grouped / depthwise, 1x1 layers on a handful of pixels).  One thread computes
+// COG consecutive output channels of one pixel; the packed weights are staged in
+// LDS as fp32 when they fit, and every input value is loaded once per thread.
+template <typename T, int COG>
+__global__ __launch_bounds__(256) void conv_direct_kernel(const lic_conv_args a, const int64_t M, const int ngroups,
+                                                          const int wlds) {
+  extern __shared__ float wsm[];
+  const T* xg = (const T*)a.x;
+  const T* wg = (const T*)a.wgt;
+  const int wtot = a.copad * a.ntaps * a.cpad;
+  if (wlds) {
+    for (int k = threadIdx.x; k < wtot; k += 256) wsm[k] = to_f(wg[k]);
+    __syncthreads();
+  }
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= M * a.co) return;
-  const int n = (int)(idx % a.co);
-  const int m = (int)(idx / a.co);
+  if (idx >= M * ngroups) return;
+  const int g = (int)(idx % ngroups);
+  const int m = (int)(idx / ngroups);
   const int mij = a.mi * a.mj;
   const int b = m / mij;
   const int rem = m - b * mij;
@@ -235,29 +259,60 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(const lic_conv_args a,
   const int j = rem - i * a.mj;
   const int cig = a.ci / a.groups;
   const int cog = a.co / a.groups;
-  const int cbase = (n / cog) * cig;
-  const T* xg = (const T*)a.x;
-  const T* wg = (const T*)a.wgt;
-  float acc = 0.f;
+  const int n0 = g * COG;
+  const int wstride = a.ntaps * a.cpad;
+  float acc[COG];
+#pragma unroll
+  for (int k = 0; k < COG; ++k) acc[k] = 0.f;
   for (int t = 0; t < a.ntaps; ++t) {
     const int iy = i * a.isy + a.dy[t], ix = j * a.isx + a.dx[t];
     if ((unsigned)iy >= (unsigned)a.h || (unsigned)ix >= (unsigned)a.w) continue;
-    const T* px = xg + ((int64_t)(b * a.h + iy) * a.w + ix) * a.ldx + cbase;
-    const T* wp = wg + ((int64_t)n * a.ntaps + t) * a.cpad;
-    for (int c = 0; c < cig; ++c) acc += apply_pro(to_f(px[c]), a.prologue) * to_f(wp[c]);
+    const T* px = xg + ((int64_t)(b * a.h + iy) * a.w + ix) * a.ldx;
+    if (a.groups == 1) {
+      for (int c = 0; c < cig; ++c) {
+        const float xv = apply_pro(to_f(px[c]), a.prologue);
+        const int wo = t * a.cpad + c;
+#pragma unroll
+        for (int k = 0; k < COG; ++k) {
+          const int n = min(n0 + k, a.copad - 1);
+          const float wv = wlds ? wsm[n * wstride + wo] : to_f(wg[(int64_t)n * wstride + wo]);
+          acc[k] += xv * wv;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < COG; ++k) {
+        const int n = min(n0 + k, a.co - 1);
+        const int cb = (n / cog) * cig;
+        for (int c = 0; c < cig; ++c) {
+          const float xv = apply_pro(to_f(px[cb + c]), a.prologue);
+          const int wo = t * a.cpad + c;
+          const float wv = wlds ? wsm[n * wstride + wo] : to_f(wg[(int64_t)n * wstride + wo]);
+          acc[k] += xv * wv;
+        }
+      }
+    }
   }
-  int64_t pix;
-  int ch;
-  out_coord(a, b, i, j, n, pix, ch);
-  const float v = conv_epilogue<T>(a, acc, n, pix, ch);
-  ((T*)a.y)[pix * a.ldy + ch] = from_f<T>(v);
-  if (a.y2) ((T*)a.y2)[pix * a.ldy2 + ch] = from_f<T>(v);
+#pragma unroll
+  for (int k = 0; k < COG; ++k) {
+    const int n = n0 + k;
+    if (n >= a.co) break;
+    int64_t pix;
+    int ch;
+    out_coord(a, b, i, j, n, pix, ch);
+    const float v = conv_epilogue<T>(a, acc[k], n, pix, ch);
+    ((T*)a.y)[pix * a.ldy + ch] = from_f<T>(v);
+    if (a.y2) ((T*)a.y2)[pix * a.ldy2 + ch] = from_f<T>(v);
+  }
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
 static int launch_mfma(const lic_conv_args& a, int M, hipStream_t s) {
   dim3 grid((M + BM - 1) / BM, a.copad / BN);
-  hipLaunchKernelGGL((conv_mfma_kernel<T, BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, s, a, M);
+  if (a.prologue == LIC_PRO_SQUARE)
+    hipLaunchKernelGGL((conv_mfma_kernel<T, BM, BN, WM, WN, LIC_PRO_SQUARE>), grid, dim3(WM * WN * 64), 0, s, a, M);
+  else
+    hipLaunchKernelGGL((conv_mfma_kernel<T, BM, BN, WM, WN, LIC_PRO_NONE>), grid, dim3(WM * WN * 64), 0, s, a, M);
   LIC_CHECK_LAUNCH();
   return 0;
 }
@@ -271,7 +326,7 @@ static int conv_dispatch(const lic_conv_args& a, hipStream_t s) {
   const int64_t out_pix = (int64_t)a.n * a.ho * a.wo;
   if (M64 >= (1LL << 31) || out_pix >= (1LL << 31)) return fail("conv: too many pixels for int32 indexing");
   const int M = (int)M64;
-  bool mfma_ok = !a.force_direct && a.groups == 1 && a.ci % EPC == 0 && a.cpad % BK == 0 &&
+  bool mfma_ok = !a.force_direct && a.groups == 1 && a.prologue != LIC_PRO_ABS && a.ci % EPC == 0 && a.cpad % BK == 0 &&
                  a.ldx % EPC == 0 && ((uintptr_t)a.x % 16 == 0) && ((uintptr_t)a.wgt % 16 == 0) &&
                  a.copad % 32 == 0 && a.ci >= EPC;
   if (mfma_ok) {
@@ -299,9 +354,19 @@ static int conv_dispatch(const lic_conv_args& a, hipStream_t s) {
       }
     }
   }
-  const int64_t total = M64 * a.co;
+  const int cog = a.co >= 16 && a.groups == 1 ? 16 : (a.co >= 4 && a.groups == 1 ? 4 : 1);
+  const int ngroups = (a.co + cog - 1) / cog;
+  const int64_t total = M64 * ngroups;
   const int64_t blocks = (total + 255) / 256;
-  hipLaunchKernelGGL((conv_direct_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, a, M64);
+  const size_t wbytes = (size_t)a.copad * a.ntaps * a.cpad * sizeof(float);
+  const int wlds = wbytes <= 48 * 1024 ? 1 : 0;
+  const size_t shm = wlds ? wbytes : 0;
+  if (cog == 16)
+    hipLaunchKernelGGL((conv_direct_kernel<T, 16>), dim3((unsigned)blocks), dim3(256), shm, s, a, M64, ngroups, wlds);
+  else if (cog == 4)
+    hipLaunchKernelGGL((conv_direct_kernel<T, 4>), dim3((unsigned)blocks), dim3(256), shm, s, a, M64, ngroups, wlds);
+  else
+    hipLaunchKernelGGL((conv_direct_kernel<T, 1>), dim3((unsigned)blocks), dim3(256), shm, s, a, M64, ngroups, wlds);
   LIC_CHECK_LAUNCH();
   return 0;
 }

@@ -150,7 +150,10 @@ def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
     """nn.Conv2d weight [co, ci/g, kh, kw] -> packed [copad][kh*kw][cpad]; pad = (top, left, bottom, right)."""
     co, cig, kh, kw = weight.shape
     pt, pl, pb, pr = pad
-    cpad = _cpad_for(cig, dtype) if groups == 1 else cig
+    # channel counts the MFMA kernel cannot take (not a multiple of one 16-byte chunk, or
+    # grouped) go to the direct kernel, which wants the weights unpadded
+    epc = 8 if dtype == torch.float16 else 4
+    cpad = _cpad_for(cig, dtype) if (groups == 1 and cig % epc == 0) else cig
     copad = _choose_copad(co)
     w = torch.zeros((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
     w[:co, :, :cig] = weight.detach().permute(0, 2, 3, 1).reshape(co, kh * kw, cig).to(dtype)

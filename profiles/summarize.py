@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace (rocpd SQLite .db or kernel_trace.csv) into a
+per-kernel stats table: calls, total / average / min / max duration, share.
+
+usage: python profiles/summarize.py <results.db | kernel_trace.csv> [--grid] [--top N]
+"""
+import collections
+import csv
+import sqlite3
+import sys
+
+
+def load(path):
+    rows = []  # (name, dur_ns, grid)
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        tabs = [r[0] for r in c.execute("select name from sqlite_master where type='table'")]
+        kd = [t for t in tabs if t.startswith("rocpd_kernel_dispatch")][0]
+        ks = [t for t in tabs if t.startswith("rocpd_info_kernel_symbol")][0]
+        q = (f"select s.kernel_name, d.end - d.start, d.grid_size_x, d.grid_size_y, d.workgroup_size_x "
+             f"from {kd} d join {ks} s on d.kernel_id = s.id")
+        for name, dur, gx, gy, wx in c.execute(q):
+            rows.append((name, dur, (gx // max(wx, 1), gy)))
+    else:
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                rows.append((r["Kernel_Name"], dur, (r.get("Grid_Size_X"), r.get("Grid_Size_Y"))))
+    return rows
+
+
+def short(name):
+    import re
+    n = re.sub(r"\(.*", "", name)
+    return n[:110]
+
+
+def main():
+    path = sys.argv[1]
+    by_grid = "--grid" in sys.argv
+    top = 40
+    if "--top" in sys.argv:
+        top = int(sys.argv[sys.argv.index("--top") + 1])
+    rows = load(path)
+    agg = collections.OrderedDict()
+    for name, dur, grid in rows:
+        key = (short(name), grid) if by_grid else short(name)
+        a = agg.setdefault(key, [0, 0, None, 0])
+        a[0] += 1
+        a[1] += dur
+        a[2] = dur if a[2] is None else min(a[2], dur)
+        a[3] = max(a[3], dur)
+    total = sum(a[1] for a in agg.values())
+    print(f"# kernels: {len(rows)} dispatches, total {total / 1e6:.3f} ms")
+    print(f"{'calls':>7} {'total_ms':>10} {'avg_us':>10} {'min_us':>9} {'max_us':>9} {'pct':>6}  kernel")
+    for key, (n, s, mn, mx) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"{n:7d} {s / 1e6:10.3f} {s / n / 1e3:10.2f} {mn / 1e3:9.2f} {mx / 1e3:9.2f} {100 * s / total:6.2f}  {key}")
+
+
+if __name__ == "__main__":
+    main()
