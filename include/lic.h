@@ -80,6 +80,7 @@ typedef struct lic_conv_args {
   const void* r2; int32_t ldr2;
   int32_t out_shuffle;               /* 0 or 2 */
   int32_t force_direct;              /* testing: force the non-MFMA kernel */
+  int32_t force_mfma_generic;        /* testing: skip the spatial-tile (halo) kernel */
 } lic_conv_args;
 
 /* Convolution / linear layer (nn.Conv2d, nn.ConvTranspose2d phase, nn.Linear as

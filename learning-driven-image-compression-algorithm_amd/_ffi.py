@@ -54,6 +54,7 @@ class ConvArgs(ctypes.Structure):
         ("r2", _vp), ("ldr2", _i32),
         ("out_shuffle", _i32),
         ("force_direct", _i32),
+        ("force_mfma_generic", _i32),
     ]
 
 

@@ -201,35 +201,19 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
   // activation, residual / gate / GDN / half-tanh, channel-offset + shuffle
   // addressing, contiguous stores.
   float* ct = (float*)smem + wave * (32 * 33);
-  const int erow = lane >> 1, ecol = (lane & 1) * 16;
-  T* __restrict__ yg = (T*)a.y;
-  T* __restrict__ y2g = (T*)a.y2;
+  const bool vec_ok = epi_vec_ok<T>(a);
+#pragma nounroll
+  for (int q = 0; q < TM * TN; ++q) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+    for (int qq = 0; qq < TM * TN; ++qq)
+      if (qq == q) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[i][j][r];
-      __syncthreads();
-      const int base = rowpix[wm * WTM + i * 32 + erow];
-      const int nb = n0 + wn * WTN + j * 32 + ecol;
-      if (base >= 0) {
-        for (int c = 0; c < 16; ++c) {
-          const int n = nb + c;
-          if (n >= a.co) break;
-          int64_t pix = base;
-          int ch = n;
-          if (a.out_shuffle == 2) {
-            pix += ((n >> 1) & 1) * a.wo + (n & 1);
-            ch = n >> 2;
-          }
-          const float v = conv_epilogue<T>(a, ct[erow * 33 + ecol + c], n, pix, ch);
-          yg[pix * a.ldy + ch] = from_f<T>(v);
-          if (y2g) y2g[pix * a.ldy2 + ch] = from_f<T>(v);
-        }
+        for (int r = 0; r < 16; ++r)
+          ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r];
       }
-      __syncthreads();
-    }
+    __syncthreads();
+    epilogue_tile<T>(a, ct, rowpix + wm * WTM + (q / TN) * 32, n0 + wn * WTN + (q % TN) * 32, lane, vec_ok);
+    __syncthreads();
   }
 }
 
@@ -329,6 +313,10 @@ static int conv_dispatch(const lic_conv_args& a, hipStream_t s) {
   bool mfma_ok = !a.force_direct && a.groups == 1 && a.prologue != LIC_PRO_ABS && a.ci % EPC == 0 && a.cpad % BK == 0 &&
                  a.ldx % EPC == 0 && ((uintptr_t)a.x % 16 == 0) && ((uintptr_t)a.wgt % 16 == 0) &&
                  a.copad % 32 == 0 && a.ci >= EPC;
+  if (mfma_ok && !a.force_mfma_generic) {
+    int st = 0;
+    if (conv_halo_dispatch<T>(a, s, st)) return st;
+  }
   if (mfma_ok) {
     int BN = 0;
     const int cands[5] = {192, 128, 96, 64, 32};

@@ -209,7 +209,7 @@ def _ptr(a: Optional[Act]):
 def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT_NONE, slope: float = 0.01,
          epi: int = _ffi.EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
          y2: Optional[Act] = None, prologue: int = _ffi.PRO_NONE, out_hw=None, shuffle: bool = False,
-         force_direct: bool = False) -> Act:
+         force_direct: bool = False, force_generic: bool = False) -> Act:
     """Run one ConvPack launch. For convT phases `out` (full map) must be given."""
     if x.c != pk.ci:
         raise ValueError(f"conv: input has {x.c} channels, weights expect {pk.ci}")
@@ -252,6 +252,7 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     a.r2, a.ldr2 = _ptr(r2)
     a.out_shuffle = 2 if shuffle else 0
     a.force_direct = 1 if force_direct else 0
+    a.force_mfma_generic = 1 if force_generic else 0
     check(_lib().lic_conv2d_fwd(ctypes.byref(a), stream_handle()))
     return out
 

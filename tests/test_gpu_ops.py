@@ -321,3 +321,36 @@ def test_loud_failure_on_bad_args():
     a = Fn.Act(torch.randn(1, 6, 6, 24, device=DEV))
     with pytest.raises(LicError):
         Fn.win_attn(a, 8, 3, 4, 0, torch.zeros(49, 3, device=DEV), 3, 1, 0, False, 1.0)  # 6 % 4 != 0
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("cin,cout,k,s,pad,B,H", [
+    (192, 192, 3, 1, (1, 1, 1, 1), 16, 64),   # Win_noShift_Attention conv3x3 @ H/4
+    (192, 192, 7, 1, (3, 3, 3, 3), 16, 64),   # conv7x7 (tap groups)
+    (192, 192, 5, 2, (1, 1, 2, 2), 8, 128),   # ZeroPad2d((1,2,1,2)) + conv5x5 s2
+    (192, 192, 3, 2, (1, 1, 1, 1), 8, 96),    # RBWS conv1 (stride 2), ragged tiles (96/2=48)
+    (96, 96, 3, 1, (1, 1, 1, 1), 16, 50),     # ragged tile edges, BN=128 pad
+])
+def test_conv_halo_matches_generic(dtype, cin, cout, k, s, pad, B, H):
+    """The spatial-tile (halo) kernel and the generic implicit-GEMM kernel agree."""
+    from lic_amd.layers import Conv2d
+    import lic_amd.functional as Fn
+    torch.manual_seed(15)
+    m = Conv2d(cin, cout, k, s, 0).to(DEV)
+    x = _act(torch.randn(B, cin, H, H), dtype)
+    pk = m.packed(dtype, pad)
+    a = Fn.conv(x, pk)
+    b = Fn.conv(x, pk, force_generic=True)
+    _close(a.nchw(), b.nchw(), dtype, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_conv_transpose_halo_matches_cpu(dtype):
+    """s_model's ZeroPad2d((1,0,1,0)) + ConvTranspose2d(5, 2, 3, op=1) at a size that takes the halo kernel."""
+    from lic_amd.layers import ConvTranspose2d
+    torch.manual_seed(16)
+    m = ConvTranspose2d(192, 192, 5, 2, 3, output_padding=1).to(DEV)
+    x = torch.randn(8, 192, 32, 32)
+    out = m.run(_act(x, dtype), prepad=(1, 1)).nchw()
+    ref = F.conv_transpose2d(F.pad(x, (1, 0, 1, 0)), m.weight.cpu(), m.bias.cpu(), 2, 3, 1)
+    _close(out, ref, dtype)

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the conv kernels on the a_model / s_model hot shapes.
+
+Times each shape with the automatic kernel choice and with the generic implicit-GEMM
+kernel (force_generic), interleaved in one process (HIP events on the launch
+stream), and prints TFLOP/s against the dense MFMA peak of the dtype.
+usage: python tools/conv_bench.py [--dtype fp16|fp32] [--batch 32] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PEAK = {"fp16": 2516.6, "fp32": 157.3}
+
+# (name, cin, cout, k, stride, pad(t,l,b,r), H_in)   at 256x256 input
+SHAPES = [
+    ("wnsa3x3@64", 192, 192, 3, 1, (1, 1, 1, 1), 64),
+    ("wnsa7x7@64", 192, 192, 7, 1, (3, 3, 3, 3), 64),
+    ("rbws_conv2@128", 192, 192, 3, 1, (1, 1, 1, 1), 128),
+    ("conv5x5s2@128", 192, 192, 5, 2, (1, 1, 2, 2), 128),
+    ("qkv1x1@64", 192, 576, 1, 1, (0, 0, 0, 0), 64),
+    ("rbneck3x3_96@64", 96, 96, 3, 1, (1, 1, 1, 1), 64),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="fp16")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    import lic_amd.functional as Fn
+    from lic_amd.layers import Conv2d
+    dt = torch.float16 if args.dtype == "fp16" else torch.float32
+    dev = "cuda"
+    st = torch.cuda.current_stream()
+    for name, ci, co, k, s, pad, H in SHAPES:
+        m = Conv2d(ci, co, k, s, 0).to(dev)
+        x = Fn.Act(torch.randn(args.batch, H, H, ci, device=dev).to(dt))
+        pk = m.packed(dt, pad)
+        Ho, Wo = Fn.conv_out_hw(H, H, pk)
+        out = Fn.Act.empty(args.batch, Ho, Wo, co, dt, dev)
+        flops = 2.0 * args.batch * Ho * Wo * co * ci * k * k
+        res = {}
+        for variant in ("auto", "generic", "auto", "generic"):
+            kw = dict(force_generic=(variant == "generic"))
+            for _ in range(2):
+                Fn.conv(x, pk, out, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(args.iters):
+                Fn.conv(x, pk, out, **kw)
+            e1.record(st)
+            e1.synchronize()
+            t = e0.elapsed_time(e1) / 1e3 / args.iters
+            res.setdefault(variant, []).append(t)
+        line = f"{name:18s} {flops / 1e9:8.1f} GFLOP"
+        for v, ts in res.items():
+            t = min(ts)
+            tf = flops / t / 1e12
+            line += f" | {v:7s} {t * 1e6:8.1f} us {tf:7.1f} TF/s ({100 * tf / PEAK[args.dtype]:5.1f}%)"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
