@@ -141,6 +141,8 @@ def main():
     ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     ap.add_argument("--no-extras", action="store_true", help="skip cpu baseline / parity / fp32 legs")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--profile", action="store_true",
+                    help="only warm-up + timed replays (for rocprofv3 per-forward kernel breakdowns)")
     args = ap.parse_args()
 
     world = _env_int("WORLD_SIZE", 1)
@@ -190,6 +192,10 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     result = None
+    if args.profile:
+        if rank == 0:
+            print(json.dumps({"profile_run": True, "value": round(value, 2), "ms_per_step": round(ms_per_step, 3)}))
+        return
     if rank == 0:
         flops, tk = dominant_kernel_roofline(dtype, args.batch, device)
         peak = FP16_PEAK_TFLOPS if dtype == torch.float16 else FP32_PEAK_TFLOPS

@@ -171,9 +171,16 @@ int lic_psnr_finalize(const double* sqerr_partials, int32_t n, int32_t parts_per
                       double count, float* v_mse, float* v_psnr, lic_stream_t stream);
 
 /* Layout / elementwise helpers. */
-/* NCHW fp32 -> NHWC view of dtype (and back). */
+/* NCHW fp32 -> NHWC view of dtype (and back); channels [c, cpad) of the
+ * destination are zero-filled (cpad = c for a plain conversion). */
 int lic_nchw_to_nhwc(int32_t dtype, const float* x, int32_t n, int32_t c, int32_t h, int32_t w,
-                     void* y, int32_t ldy, lic_stream_t stream);
+                     void* y, int32_t ldy, int32_t cpad, lic_stream_t stream);
+/* Fused ResidualBottleneck(3) (net_ga.py:89-103 with N = 3: 1x1 3->1, GELU,
+ * 3x3 1->1, GELU, 1x1 1->3, + x) in one pass; params = w1[3], b1, w2[9], b2,
+ * w3[3], b3[3] (fp32).  Writes all ldy channels of each output pixel
+ * (channels 3.. zero) so the 3->192 convolutions can run on MFMA. */
+int lic_rb3_fwd(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t ldx,
+                const float* params, void* y, int32_t ldy, lic_stream_t stream);
 int lic_nhwc_to_nchw(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t c,
                      int32_t ldx, float* y, lic_stream_t stream);
 /* y = a + b (views, same geometry). */

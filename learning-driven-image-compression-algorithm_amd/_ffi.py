@@ -23,7 +23,7 @@ EXPORTED_SYMBOLS = (
     "lic_conv2d_fwd", "lic_gdn_prepare", "lic_win_attn_fwd", "lic_layernorm_fwd",
     "lic_gauss_rate_fwd", "lic_quantize_median", "lic_bpp_finalize", "lic_syntax_recon_fwd",
     "lic_psnr_finalize", "lic_nchw_to_nhwc", "lic_nhwc_to_nchw", "lic_add", "lic_copy",
-    "lic_avgpool", "lic_last_error", "lic_version", "lic_device_arch",
+    "lic_avgpool", "lic_rb3_fwd", "lic_last_error", "lic_version", "lic_device_arch",
 )
 
 
@@ -115,7 +115,8 @@ def load():
         "lic_bpp_finalize": [V, I, D, V, V, V],
         "lic_syntax_recon_fwd": [I, V, I, I, I, I, I, V, I, V, V, V, I, V],
         "lic_psnr_finalize": [V, I, I, D, V, V, V],
-        "lic_nchw_to_nhwc": [I, V, I, I, I, I, V, I, V],
+        "lic_nchw_to_nhwc": [I, V, I, I, I, I, V, I, I, V],
+        "lic_rb3_fwd": [I, V, I, I, I, I, V, V, I, V],
         "lic_nhwc_to_nchw": [I, V, I, I, I, I, I, V, V],
         "lic_add": [I, V, I, V, I, I, I, V, I, V],
         "lic_copy": [I, V, I, I, I, I, V, I, V],

@@ -7,18 +7,18 @@ namespace lic {
 // coalesced along w for each channel plane via a 2-D grid.
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int n, int c, int h, int w, T* __restrict__ y,
-                                    int ldy) {
+                                    int ldy, int cpad) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = (int64_t)n * c * h * w;
+  const int64_t total = (int64_t)n * cpad * h * w;
   if (idx >= total) return;
-  // idx enumerates NHWC order: ((b*h + yy)*w + xx)*c + k
-  const int k = (int)(idx % c);
-  const int64_t pix = idx / c;
+  // idx enumerates NHWC order: ((b*h + yy)*w + xx)*cpad + k; channels [c, cpad) are zero-filled
+  const int k = (int)(idx % cpad);
+  const int64_t pix = idx / cpad;
   const int xx = (int)(pix % w);
   const int64_t t = pix / w;
   const int yy = (int)(t % h);
   const int b = (int)(t / h);
-  y[pix * ldy + k] = from_f<T>(x[(((int64_t)b * c + k) * h + yy) * w + xx]);
+  y[pix * ldy + k] = k < c ? from_f<T>(x[(((int64_t)b * c + k) * h + yy) * w + xx]) : from_f<T>(0.f);
 }
 
 template <typename T>
@@ -93,12 +93,13 @@ using namespace lic;
 static inline unsigned nblk(int64_t total) { return (unsigned)((total + 255) / 256); }
 
 extern "C" int lic_nchw_to_nhwc(int32_t dtype, const float* x, int32_t n, int32_t c, int32_t h, int32_t w, void* y,
-                                int32_t ldy, lic_stream_t stream) {
-  const int64_t total = (int64_t)n * c * h * w;
+                                int32_t ldy, int32_t cpad, lic_stream_t stream) {
+  if (cpad < c || cpad > ldy) return fail("nchw_to_nhwc: need c <= cpad <= ldy");
+  const int64_t total = (int64_t)n * cpad * h * w;
   if (!total) return 0;
   DISPATCH_T(dtype, "nchw_to_nhwc",
              hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(nblk(total)), dim3(256), 0, (hipStream_t)stream, x, n, c,
-                                h, w, (T*)y, ldy));
+                                h, w, (T*)y, ldy, cpad));
   LIC_CHECK_LAUNCH();
   return 0;
 }

@@ -36,15 +36,18 @@ def _lib():
 
 
 class Act:
-    """NHWC activation view: channels [c0, c0 + c) of a contiguous [B, H, W, Ctot] tensor."""
-    __slots__ = ("t", "c0", "c")
+    """NHWC activation view: channels [c0, c0 + c) of a contiguous [B, H, W, Ctot] tensor.
+    ``zpad`` >= c: channels [c0 + c, c0 + zpad) are known to be zero (lets a Cin=3 layer
+    run as a zero-padded Cin=8/4 MFMA convolution)."""
+    __slots__ = ("t", "c0", "c", "zpad")
 
-    def __init__(self, t: torch.Tensor, c0: int = 0, c: Optional[int] = None):
+    def __init__(self, t: torch.Tensor, c0: int = 0, c: Optional[int] = None, zpad: Optional[int] = None):
         if t.dim() != 4 or not t.is_contiguous():
             raise ValueError("Act expects a contiguous [B, H, W, C] tensor")
         self.t = t
         self.c0 = c0
         self.c = t.shape[3] - c0 if c is None else c
+        self.zpad = self.c if zpad is None else zpad
 
     @property
     def B(self):
@@ -88,16 +91,19 @@ class Act:
         return Act(torch.empty((B, H, W, C), dtype=dtype, device=device))
 
     @staticmethod
-    def from_nchw(x: torch.Tensor, dtype: Optional[torch.dtype] = None) -> "Act":
-        """NCHW-logical tensor -> NHWC Act (zero copy when already channels_last of the dtype)."""
+    def from_nchw(x: torch.Tensor, dtype: Optional[torch.dtype] = None, pad16: bool = False) -> "Act":
+        """NCHW-logical tensor -> NHWC Act (zero copy when already channels_last of the dtype).
+        pad16: store pixels padded with zero channels to a 16-byte multiple (Act.zpad)."""
         dtype = dtype or x.dtype
         t = x.permute(0, 2, 3, 1)
-        if t.dtype == dtype and t.is_contiguous():
+        if t.dtype == dtype and t.is_contiguous() and not pad16:
             return Act(t)
         if x.dtype == torch.float32 and x.is_contiguous():
             B, C, H, W = x.shape
-            out = Act.empty(B, H, W, C, dtype, x.device)
-            check(_lib().lic_nchw_to_nhwc(dtype_id(dtype), x.data_ptr(), B, C, H, W, out.ptr, out.ld,
+            epc = 16 // torch.empty((), dtype=dtype).element_size()
+            cp = -(-C // epc) * epc if pad16 else C
+            out = Act(torch.empty((B, H, W, cp), dtype=dtype, device=x.device), 0, C, cp)
+            check(_lib().lic_nchw_to_nhwc(dtype_id(dtype), x.data_ptr(), B, C, H, W, out.ptr, out.ld, cp,
                                           stream_handle()))
             return out
         return Act(t.to(dtype).contiguous())
@@ -146,22 +152,24 @@ def _cpad_for(ci: int, dtype: torch.dtype) -> int:
 
 
 def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad, dtype: torch.dtype,
-                groups: int = 1) -> ConvPack:
-    """nn.Conv2d weight [co, ci/g, kh, kw] -> packed [copad][kh*kw][cpad]; pad = (top, left, bottom, right)."""
+                groups: int = 1, cin_to: Optional[int] = None) -> ConvPack:
+    """nn.Conv2d weight [co, ci/g, kh, kw] -> packed [copad][kh*kw][cpad]; pad = (top, left, bottom, right).
+    cin_to: treat the input as cin_to channels (extra channels known zero; zero weights)."""
     co, cig, kh, kw = weight.shape
     pt, pl, pb, pr = pad
+    cin = cig if cin_to is None else cin_to
     # channel counts the MFMA kernel cannot take (not a multiple of one 16-byte chunk, or
     # grouped) go to the direct kernel, which wants the weights unpadded
     epc = 8 if dtype == torch.float16 else 4
-    cpad = _cpad_for(cig, dtype) if (groups == 1 and cig % epc == 0) else cig
+    cpad = _cpad_for(cin, dtype) if (groups == 1 and cin % epc == 0) else cin
     copad = _choose_copad(co)
     w = torch.zeros((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
     w[:co, :, :cig] = weight.detach().permute(0, 2, 3, 1).reshape(co, kh * kw, cig).to(dtype)
     dy = [ky - pt for ky in range(kh) for kx in range(kw)]
     dx = [kx - pl for ky in range(kh) for kx in range(kw)]
     b = bias.detach().float().contiguous() if bias is not None else None
-    return ConvPack(w=w, bias=b, ci=cig * groups, co=co, dy=dy, dx=dx, groups=groups, stride=stride,
-                    pad=(pt, pl, pb, pr), kh=kh, kw=kw)
+    return ConvPack(w=w, bias=b, ci=cin * groups if cin_to is None else cin, co=co, dy=dy, dx=dx, groups=groups,
+                    stride=stride, pad=(pt, pl, pb, pr), kh=kh, kw=kw)
 
 
 def pack_conv_transpose2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
@@ -304,6 +312,18 @@ def layernorm(x: Act, weight: torch.Tensor, bias: torch.Tensor, eps: float, out:
         out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)
     check(_lib().lic_layernorm_fwd(dtype_id(x.dtype), x.ptr, x.npix, x.c, x.ld, weight.data_ptr(), bias.data_ptr(),
                                    eps, out.ptr, out.ld, stream_handle()))
+    return out
+
+
+def rb3(x: Act, params: torch.Tensor, out: Optional[Act] = None) -> Act:
+    """Fused ResidualBottleneck(3); the output pixels are zero-padded to 16 bytes (Act.zpad)."""
+    if x.c != 3:
+        raise ValueError("rb3 expects a 3-channel view")
+    if out is None:
+        epc = 16 // x.t.element_size()
+        out = Act(torch.empty((x.B, x.H, x.W, epc), dtype=x.dtype, device=x.t.device), 0, 3, epc)
+    check(_lib().lic_rb3_fwd(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.ld, params.data_ptr(), out.ptr, out.ld,
+                             stream_handle()))
     return out
 
 

@@ -73,9 +73,22 @@ class ResidualBottleneck(nn.Module):
                                     conv1x1(N // 2, N))
 
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        if x.c == 3 and self.branch[0].out_channels == 1 and out is None:
+            return Fn.rb3(x, self._rb3_params())                 # whole block in one pass
         t = self.branch[0].run(x, act=ACT_GELU)
         t = self.branch[2].run(t, act=ACT_GELU)
         return self.branch[4].run(t, out, r1=x)
+
+    def _rb3_params(self) -> torch.Tensor:
+        b = self.branch
+        ps = (b[0].weight, b[0].bias, b[2].weight, b[2].bias, b[4].weight, b[4].bias)
+        key = tuple((p.data_ptr(), p._version) for p in ps)
+        c = self.__dict__.get("_rb3_cache")
+        if c is None or c[0] != key:
+            flat = torch.cat([p.detach().float().reshape(-1) for p in ps]).contiguous()
+            c = (key, flat)
+            self.__dict__["_rb3_cache"] = c
+        return c[1]
 
     def forward(self, x):
         return self.run(Act.from_nchw(x)).nchw()

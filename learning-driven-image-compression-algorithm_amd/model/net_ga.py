@@ -409,12 +409,36 @@ class Net(nn.Module):
         self.h_scale_s = mk()
 
     def _hyper(self, z3: Act, means_out: Act, scales_out: Act):
-        """net_ga.py:993-1007: z = h_a(y); z_hat = round(z - m) + m; scales/means = h_*_s(z_hat)."""
+        """net_ga.py:993-1007: z = h_a(y); z_hat = round(z - m) + m; scales/means = h_*_s(z_hat)
+        (the two hyper-synthesis stacks run concurrently)."""
         z = _run_seq_gelu(self.h_a, z3)
-        z_hat = Fn.quantize_median(z, self.entropy_bottleneck.medians_flat().to(z.t.device))
-        _run_seq_gelu(self.h_scale_s, z_hat, scales_out)
+        z_hat = Fn.quantize_median(z, self._medians(z.t.device))
+        main = torch.cuda.current_stream(z.t.device)
+        side = self._side_stream(z.t.device, 1)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            _run_seq_gelu(self.h_scale_s, z_hat, scales_out)
         _run_seq_gelu(self.h_mean_s, z_hat, means_out)
+        main.wait_stream(side)
         return z, z_hat
+
+    def _medians(self, device):
+        """EntropyBottleneck._get_medians() flattened to [C] fp32 (cached per parameter version)."""
+        q = self.entropy_bottleneck.quantiles
+        key = (q.data_ptr(), q._version, str(device))
+        c = self.__dict__.get("_med_cache")
+        if c is None or c[0] != key:
+            c = (key, self.entropy_bottleneck.medians_flat().to(device))
+            self.__dict__["_med_cache"] = c
+        return c[1]
+
+    def _side_stream(self, device, k: int = 0):
+        """Per-device side streams for the independent branches of the graph."""
+        ss = self.__dict__.setdefault("_lic_streams", {})
+        key = (str(device), k)
+        if key not in ss:
+            ss[key] = torch.cuda.Stream(device=device)
+        return ss[key]
 
     _shared_support = False  # net_unet_ha_hs: latent_scales == latent_means
 
@@ -463,15 +487,23 @@ class Net(nn.Module):
         x_in = inputs.contiguous().float()
         B, _, H, W = x_in.shape
         dev, dt = x_in.device, self.dtype
-        x = Act.from_nchw(x_in, dt)
+        x = Act.from_nchw(x_in, dt, pad16=True)                   # 3 -> 16-byte zero-padded pixels
         z3 = self.a_model.run(x)                                  # net_ga.py:988
         hh, ww = z3.H, z3.W
         ns, sw = self.num_slices, 192 // self.num_slices
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+        # syntax head (net_ga.py:1010-1016, :1083) only meets the main chain at the
+        # reconstruction: it runs concurrently on a side stream (joined below)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            syn_r = self.syntax_model.run(z3.ch(0, self.M))
+            cw = self.conv_weights_gen.run(syn_r)
         # concat buffers: MS = [latent_means | y_hat_0..3], SS = [latent_scales | y_hat_0..2]
         MS = Act.empty(B, hh, ww, 192 + 192, dt, dev)
         SS = MS if self._shared_support else Act.empty(B, hh, ww, 192 + 144, dt, dev)
         z, z_hat = self._hyper(z3, MS.ch(0, 192), SS.ch(0, 192))
-        syn_r = self.syntax_model.run(z3.ch(0, self.M))            # net_ga.py:1010-1016
+        side2 = self._side_stream(dev, 1)
         LR = Act.empty(B, hh, ww, 192 + sw * 4, dt, dev)           # lrp_support (widest: 384)
         MU = Act.empty(B, hh, ww, 192, dt, dev)
         SC = Act.empty(B, hh, ww, 192, dt, dev)
@@ -481,16 +513,20 @@ class Net(nn.Module):
         partials = torch.empty((ns * nper,), dtype=torch.float64, device=dev)
         for i in range(ns):                                        # net_ga.py:1028-1062
             ci = 192 + sw * min(i, 4)
+            # the scale branch (:1042-1046) is independent of the mean branch (:1034-1040)
+            side2.wait_stream(main)
+            with torch.cuda.stream(side2):
+                ss = self.atten_scale[i][0].run(SS.ch(0, ci))
+                cs = self.cc_scale_transforms[i]
+                t = cs[0].run(ss, act=ACT_GELU)
+                t = cs[2].run(t, act=ACT_GELU)
+                sc = cs[4].run(t, out=SC.ch(sw * i, sw * (i + 1)))
             ms = self.atten_mean[i][0].run(MS.ch(0, ci), out=LR.ch(0, ci))
             cm = self.cc_mean_transforms[i]
             t = cm[0].run(ms, act=ACT_GELU)
             t = cm[2].run(t, act=ACT_GELU)
             mu = cm[4].run(t, out=MU.ch(sw * i, sw * (i + 1)))
-            ss = self.atten_scale[i][0].run(SS.ch(0, ci))
-            cs = self.cc_scale_transforms[i]
-            t = cs[0].run(ss, act=ACT_GELU)
-            t = cs[2].run(t, act=ACT_GELU)
-            sc = cs[4].run(t, out=SC.ch(sw * i, sw * (i + 1)))
+            main.wait_stream(side2)
             yq = LR.ch(ci, ci + sw)
             Fn.gauss_rate(z3.ch(sw * i, sw * (i + 1)), mu, sc, partials, i * nper, yq=yq,
                           symbols=Act(SYM, sw * i, sw),
@@ -504,7 +540,7 @@ class Net(nn.Module):
             lr[4].run(t, out=MS.ch(192 + sw * i, 192 + sw * (i + 1)), epi=EPI_HALF_TANH, r2=yq, y2=y2)
         y_hat = MS.ch(192, 384)
         x_tilde = self.s_model.run(y_hat)                          # net_ga.py:1078
-        cw = self.conv_weights_gen.run(syn_r)                      # net_ga.py:1083
+        main.wait_stream(side)                                     # syntax head joined
         x_rec = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
         ppi = max(1, min(64, -(-(H * W) // 4096)))
         sq_parts = torch.empty((B * ppi,), dtype=torch.float64, device=dev)

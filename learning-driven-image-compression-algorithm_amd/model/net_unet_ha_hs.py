@@ -31,6 +31,6 @@ class Net(_NetGA):
 
     def _hyper(self, z3: Act, means_out: Act, scales_out: Act):
         z, middle_x, down_x1, inp = self.h_a.run(z3)                     # :880
-        z_hat = Fn.quantize_median(z, self.entropy_bottleneck.medians_flat().to(z.t.device))  # :885-889
+        z_hat = Fn.quantize_median(z, self._medians(z.t.device))          # :885-889
         self.h_s.run(z_hat, middle_x, down_x1, inp, out=means_out)       # :892 / :895 (identical)
         return z, z_hat
