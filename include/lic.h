@@ -118,6 +118,7 @@ typedef struct lic_attn_args {
   int32_t mask_kind;   /* 0 none, 1 WBA regions (-100), 2 WMSA last row/col (-inf) */
   int32_t scale_after; /* 0: q*scale before dot, 1: dot*scale */
   float scale;         /* head_dim ** -0.5 (as the reference's Python float, cast to fp32) */
+  int32_t force_valu;  /* 1: skip the MFMA kernel (ws 8, head_dim <= 32) - testing only */
 } lic_attn_args;
 int lic_win_attn_fwd(const lic_attn_args* a, lic_stream_t stream);
 

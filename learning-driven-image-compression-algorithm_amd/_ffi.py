@@ -66,6 +66,7 @@ class AttnArgs(ctypes.Structure):
         ("heads", _i32), ("ws", _i32), ("shift", _i32),
         ("table", _vp), ("tab_sr", _i32), ("tab_sh", _i32),
         ("mask_kind", _i32), ("scale_after", _i32), ("scale", _f32),
+        ("force_valu", _i32),
     ]
 
 

@@ -160,8 +160,12 @@ static int attn_dispatch_d(const lic_attn_args& a, hipStream_t s) {
   }
 }
 
+int win_attn_mfma_dispatch(const lic_attn_args& a, hipStream_t s, int& status);
+
 template <typename T>
 static int attn_dispatch(const lic_attn_args& a, hipStream_t s) {
+  int status = 0;
+  if (win_attn_mfma_dispatch(a, s, status)) return status;
   switch (a.ws) {
     case 8: return attn_dispatch_d<T, 64>(a, s);
     case 4: return attn_dispatch_d<T, 16>(a, s);

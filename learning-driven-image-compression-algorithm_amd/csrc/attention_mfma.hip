@@ -1,0 +1,232 @@
+// Window attention on MFMA for 8x8 windows (64 tokens) and head_dim <= 32 (gfx950).
+//
+// One wave per (image, window, head); a workgroup holds 4 heads of one window.
+// Scores are computed transposed, S^T = K Q^T (keys on the accumulator rows,
+// queries on the lanes), so the softmax over keys of a query is a reduction over
+// the lane's own registers plus one exchange with lane^32, and the probability
+// registers feed O^T = V^T P^T directly as the B operand (the guide's
+// "accumulator as the next MFMA's operand": registers 8s..8s+7 are k-step s with
+// the permuted key order 16s + 8(e>>2) + 4h + (e&3); V^T is staged in LDS and read
+// in that same order).  O^T puts 4 consecutive channels of one query in a lane,
+// stored as 8/16-byte runs at the query's original (un-rolled) pixel.
+//   fp16: v_mfma_f32_32x32x16_f16 (head_dim padded to 16/32 with zeros)
+//   fp32: v_mfma_f32_32x32x2_f32 (exact fp32 products)
+// Score = dot*scale + rel-pos bias (+ -100 region mask for WBA, -inf last
+// row/column mask for WMSA), softmax as max / exp(s-max) / sum / divide.
+#include "lic_common.h"
+
+namespace lic {
+
+constexpr int AT_N = 64;   // tokens per window (ws = 8)
+constexpr int VT_LD = 68;  // padded row (elements) of the V^T staging image
+
+template <typename T>
+__global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int d = a.c / a.heads;
+  constexpr int ws = 8;
+  const int nwx = a.w / ws, nwy = a.h / ws;
+  const int hgroups = (a.heads + 3) / 4;
+  int bid = blockIdx.x;
+  const int hg = bid % hgroups;
+  bid /= hgroups;
+  const int wx = bid % nwx;
+  bid /= nwx;
+  const int wy = bid % nwy;
+  const int b = bid / nwy;
+  const int h = hg * 4 + wave;
+  const bool active = h < a.heads;
+  const int hc = active ? h : 0;
+
+  __shared__ __attribute__((aligned(16))) T vT[4][32 * VT_LD];
+  __shared__ float tab[4][(2 * ws - 1) * (2 * ws - 1)];
+  __shared__ int pixs[AT_N];
+
+  // token t -> original pixel (roll(-shift) + window_partition as addressing)
+  if (threadIdx.x < AT_N) {
+    const int t = threadIdx.x;
+    int py = wy * ws + t / ws + a.shift, px = wx * ws + t % ws + a.shift;
+    if (py >= a.h) py -= a.h;
+    if (px >= a.w) px -= a.w;
+    pixs[t] = (b * a.h + py) * a.w + px;
+  }
+  for (int k = lane; k < (2 * ws - 1) * (2 * ws - 1); k += 64) tab[wave][k] = a.table[k * a.tab_sr + hc * a.tab_sh];
+  __syncthreads();
+
+  const T* qkv = (const T*)a.qkv;
+  const int64_t ldq = a.ldqkv;
+  const int qoff = hc * d, koff = a.c + hc * d, voff = 2 * a.c + hc * d;
+  // V^T staging: lane t writes V[t][0..31] (zeros beyond d) into vT[c][t]
+  {
+    const T* vp = qkv + (int64_t)pixs[lane] * ldq + voff;
+    for (int c = 0; c < 32; ++c) vT[wave][c * VT_LD + lane] = c < d ? vp[c] : from_f<T>(0.f);
+  }
+  __syncthreads();
+
+  // fp32 keeps the reference's order (q*scale before the dot unless scale_after);
+  // fp16 operands stay unscaled and the scale is applied to the fp32 dot
+  const float pre = (sizeof(T) == 4 && !a.scale_after) ? a.scale : 1.f;
+  const float scale = (sizeof(T) == 4 && !a.scale_after) ? 1.f : a.scale;
+  floatx16 S[2][2];  // [key tile][query tile]
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[x][y][r] = 0.f;
+
+  if constexpr (sizeof(T) == 2) {
+    // fragments straight from the qkv map: lane (row, h) holds channels 16s + 8h .. +7
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = 16 * s + 8 * lh;
+      if (16 * s >= d) break;
+      half8 kf[2], qf[2];
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int tok = 32 * t2 + lr;
+        half8 z = {};
+        kf[t2] = ch < d ? *(const half8*)(qkv + (int64_t)pixs[tok] * ldq + koff + ch) : z;
+        qf[t2] = ch < d ? *(const half8*)(qkv + (int64_t)pixs[tok] * ldq + qoff + ch) : z;
+      }
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+          S[tj][ti] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[tj], qf[ti], S[tj][ti], 0, 0, 0);
+    }
+  } else {
+    for (int k = 0; k < d; k += 2) {
+      const int ch = k + lh;
+      float kf[2], qf[2];
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int tok = 32 * t2 + lr;
+        kf[t2] = ch < d ? to_f(qkv[(int64_t)pixs[tok] * ldq + koff + ch]) : 0.f;
+        qf[t2] = ch < d ? to_f(qkv[(int64_t)pixs[tok] * ldq + qoff + ch]) * pre : 0.f;
+      }
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+          S[tj][ti] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[tj], qf[ti], S[tj][ti], 0, 0, 0);
+    }
+  }
+
+  // scale + bias + mask + softmax over keys (rows) for each query (lane column)
+  const int split = ws - a.shift;
+  const bool last_row = wy == nwy - 1, last_col = wx == nwx - 1;
+  auto reg_wba = [&](int y, int x) {
+    const int ly = y < a.h - ws ? 0 : (y < a.h - a.shift ? 1 : 2);
+    const int lx = x < a.w - ws ? 0 : (x < a.w - a.shift ? 1 : 2);
+    return ly * 3 + lx;
+  };
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti) {
+    const int i = 32 * ti + lr;
+    const int iy = i / ws, ix = i % ws;
+    const int my_reg = a.mask_kind == 1 ? reg_wba(wy * ws + iy, wx * ws + ix) : 0;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = 32 * tj + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int jy = j / ws, jx = j % ws;
+        float v = S[tj][ti][r] * scale + tab[wave][(iy - jy + ws - 1) * (2 * ws - 1) + (ix - jx + ws - 1)];
+        if (a.mask_kind == 1) {
+          if (reg_wba(wy * ws + jy, wx * ws + jx) != my_reg) v += -100.0f;
+        } else if (a.mask_kind == 2) {
+          if ((last_row && ((iy < split) != (jy < split))) || (last_col && ((ix < split) != (jx < split))))
+            v = -INFINITY;
+        }
+        S[tj][ti][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = expf(S[tj][ti][r] - mx);
+        S[tj][ti][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[tj][ti][r] *= inv;
+  }
+
+  // O^T[c][i] = sum_j V^T[c][j] P^T[j][i]
+  floatx16 O[2];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[ti][r] = 0.f;
+  const T* vrow = &vT[wave][lr * VT_LD];
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int j0 = 32 * tj + 16 * s2 + 4 * lh;
+        half8 va;
+        *(uint2*)&va = *(const uint2*)(vrow + j0);
+        *((uint2*)&va + 1) = *(const uint2*)(vrow + j0 + 8);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti) {
+          half8 pb;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pb[e] = (half_t)S[tj][ti][8 * s2 + e];
+          O[ti] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb, O[ti], 0, 0, 0);
+        }
+      }
+  } else {
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = 32 * tj + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const float va = vrow[j];
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti) O[ti] = __builtin_amdgcn_mfma_f32_32x32x2f32(va, S[tj][ti][r], O[ti], 0, 0, 0);
+      }
+  }
+  if (!active) return;
+  // lane (query i, half h) holds channels c = 8g + 4h + (0..3), g = 0..3
+  T* out = (T*)a.out;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti) {
+    const int i = 32 * ti + lr;
+    T* op = out + (int64_t)pixs[i] * a.ldo + h * d;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 8 * g + 4 * lh;
+      if (c0 >= d) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c0 + e < d) op[c0 + e] = from_f<T>(O[ti][4 * g + e]);
+    }
+  }
+}
+
+int win_attn_mfma_dispatch(const lic_attn_args& a, hipStream_t s, int& status) {
+  const int d = a.c / a.heads;
+  if (a.ws != 8 || d > 32 || d % 8 || a.ldqkv % 8 || a.force_valu) return 0;
+  if (a.dtype == LIC_F16 && ((uintptr_t)a.qkv % 16)) return 0;
+  const int64_t blocks = (int64_t)a.n * (a.h / 8) * (a.w / 8) * ((a.heads + 3) / 4);
+  if (a.dtype == LIC_F16)
+    hipLaunchKernelGGL(win_attn_mfma_kernel<half_t>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(win_attn_mfma_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  status = e == hipSuccess ? 0 : fail(std::string("attn mfma launch: ") + hipGetErrorString(e));
+  return 1;
+}
+
+}  // namespace lic

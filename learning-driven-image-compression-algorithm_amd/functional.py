@@ -293,7 +293,8 @@ def gdn(x: Act, pk: ConvPack, mode: int, out: Optional[Act] = None, r1: Optional
 
 
 def win_attn(qkv: Act, C: int, heads: int, ws: int, shift: int, table: torch.Tensor, tab_sr: int, tab_sh: int,
-             mask_kind: int, scale_after: bool, scale: float, out: Optional[Act] = None) -> Act:
+             mask_kind: int, scale_after: bool, scale: float, out: Optional[Act] = None,
+             force_valu: bool = False) -> Act:
     if out is None:
         out = Act.empty(qkv.B, qkv.H, qkv.W, C, qkv.dtype, qkv.t.device)
     a = AttnArgs()
@@ -303,6 +304,7 @@ def win_attn(qkv: Act, C: int, heads: int, ws: int, shift: int, table: torch.Ten
     a.heads, a.ws, a.shift = heads, ws, shift
     a.table, a.tab_sr, a.tab_sh = table.data_ptr(), tab_sr, tab_sh
     a.mask_kind, a.scale_after, a.scale = mask_kind, 1 if scale_after else 0, scale
+    a.force_valu = 1 if force_valu else 0
     check(_lib().lic_win_attn_fwd(ctypes.byref(a), stream_handle()))
     return out
 

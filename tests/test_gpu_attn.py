@@ -1,0 +1,102 @@
+"""GPU parity of the window-attention kernels (lic_win_attn_fwd).
+
+The 8x8-window MFMA kernel (csrc/attention_mfma.hip) and the VALU kernel
+(csrc/attention.hip, force_valu=1) are both checked against a plain PyTorch fp32
+restatement of the fused op: roll(-shift) + window_partition + softmax(q k^T * scale
++ bias + mask) v + window_reverse + roll(+shift), with the masks built by the oracle
+(layers/win_attention.py:160-181 WBA, model/Block_unet.py:197-214 WMSA).
+"""
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _attn_ref(qkv, C, heads, ws, shift, table, mask_kind, scale_after, scale):
+    """qkv: [B, H, W, >=3C] fp32; table [(2ws-1)^2, heads]."""
+    B, H, W, _ = qkv.shape
+    d = C // heads
+    x = torch.roll(qkv[..., :3 * C], shifts=(-shift, -shift), dims=(1, 2)) if shift else qkv[..., :3 * C]
+    win = R.window_partition(x.contiguous(), ws).view(-1, ws * ws, 3 * C)  # [B*nw, N, 3C]
+    q = win[..., :C].view(-1, ws * ws, heads, d).transpose(1, 2)
+    k = win[..., C:2 * C].view(-1, ws * ws, heads, d).transpose(1, 2)
+    v = win[..., 2 * C:].view(-1, ws * ws, heads, d).transpose(1, 2)
+    s = (q @ k.transpose(-2, -1)) * scale if scale_after else (q * scale) @ k.transpose(-2, -1)
+    rpi = R.relative_position_index(ws).view(-1)
+    s = s + table[rpi].view(ws * ws, ws * ws, heads).permute(2, 0, 1)[None]
+    nw = (H // ws) * (W // ws)
+    if mask_kind == 1:
+        m = R.wba_mask(H, W, ws, shift)  # [nw, N, N]
+        s = (s.view(B, nw, heads, ws * ws, ws * ws) + m[None, :, None]).view_as(s)
+    elif mask_kind == 2:
+        m = R.wmsa_mask(H // ws, W // ws, ws, shift)
+        s = s.view(B, nw, heads, ws * ws, ws * ws).masked_fill(m[None, :, None], float("-inf")).view_as(s)
+    o = torch.softmax(s, dim=-1) @ v  # [B*nw, heads, N, d]
+    o = o.transpose(1, 2).reshape(-1, ws, ws, C)
+    o = R.window_reverse(o, ws, H, W)
+    return torch.roll(o, shifts=(shift, shift), dims=(1, 2)) if shift else o
+
+
+def _run(qkv, C, heads, ws, shift, table, mask_kind, scale_after, scale, dtype, force_valu):
+    import lic_amd.functional as Fn
+    a = Fn.Act(qkv.to(DEV).to(dtype).contiguous())
+    tab = table.to(DEV).contiguous()
+    out = Fn.win_attn(a, C, heads, ws, shift, tab, heads, 1, mask_kind, scale_after, scale, force_valu=force_valu)
+    torch.cuda.synchronize()
+    return out.t[..., :C].float().cpu()
+
+
+CASES = [
+    # C, heads, ws, shift, H, W, mask_kind, scale_after
+    (192, 8, 8, 4, 16, 16, 1, False),   # Win_noShift_Attention ws 8 (net_ga.py:157), d = 24
+    (192, 8, 8, 2, 16, 24, 1, False),   # synthesis ws 8 shift 2 (net_ga.py:199)
+    (128, 8, 8, 0, 16, 8, 0, True),     # SwinBlock 'W' (d = 16)
+    (128, 8, 8, 4, 24, 16, 2, True),    # SwinBlock 'SW' (WMSA mask)
+    (256, 8, 8, 4, 16, 16, 2, True),    # d = 32
+    (48, 6, 8, 4, 8, 16, 1, False),     # d = 8, heads not a multiple of 4
+    (96, 4, 8, 0, 8, 8, 0, False),      # d = 24, single window
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("C,heads,ws,shift,H,W,mask_kind,scale_after", CASES)
+def test_mfma_attention_matches_reference(dtype, C, heads, ws, shift, H, W, mask_kind, scale_after):
+    g = torch.Generator().manual_seed(C * 7 + H + W + shift)
+    B = 2
+    qkv = torch.randn(B, H, W, 3 * C, generator=g)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g) * 0.5
+    scale = (C // heads) ** -0.5
+    qkv_q = qkv.to(dtype).float()
+    ref = _attn_ref(qkv_q, C, heads, ws, shift, table, mask_kind, scale_after, scale)
+    out = _run(qkv, C, heads, ws, shift, table, mask_kind, scale_after, scale, dtype, False)
+    valu = _run(qkv, C, heads, ws, shift, table, mask_kind, scale_after, scale, dtype, True)
+    if dtype == torch.float32:
+        torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(out, valu, rtol=1e-4, atol=1e-4)
+    else:
+        # fp16 operands and fp16 probabilities into the PV product, fp32 accumulation
+        assert (out - ref).abs().max().item() <= 1e-2 * (ref.abs().max().item() + 1e-6)
+        assert (out - valu).abs().max().item() <= 1e-2 * (ref.abs().max().item() + 1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_mfma_attention_strided_views(dtype):
+    """qkv and out as channel windows of wider NHWC buffers (ld > 3C, c0 > 0)."""
+    import lic_amd.functional as Fn
+    C, heads, ws, shift, H, W = 192, 8, 8, 4, 16, 16
+    g = torch.Generator().manual_seed(3)
+    big = torch.randn(1, H, W, 3 * C + 64, generator=g)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g) * 0.5
+    scale = (C // heads) ** -0.5
+    qkv = Fn.Act(big.to(DEV).to(dtype).contiguous(), 32, 3 * C)
+    out_buf = torch.full((1, H, W, C + 40), 7.0, device=DEV, dtype=dtype)
+    out = Fn.Act(out_buf, 16, C)
+    Fn.win_attn(qkv, C, heads, ws, shift, table.to(DEV), heads, 1, 1, False, scale, out=out)
+    ref = _attn_ref(big[..., 32:32 + 3 * C].to(dtype).float(), C, heads, ws, shift, table, 1, False, scale)
+    got = out_buf[..., 16:16 + C].float().cpu()
+    tol = 1e-4 if dtype == torch.float32 else 1e-2 * ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= tol
+    assert out_buf[..., :16].eq(7).all() and out_buf[..., 16 + C:].eq(7).all()
