@@ -30,10 +30,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
   constexpr int A_CH = BM * 4, B_CH = BN * 4;
   constexpr int A_PT = (A_CH + NT - 1) / NT, B_PT = (B_CH + NT - 1) / NT;
   constexpr int BUF = (BM + BN) * 64;
+  static_assert(WM * WN * 32 * 33 * 4 <= 2 * BUF, "epilogue slots overlap rowpix / bias");
 
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + BM * 4 + 2 * LIC_MAX_TAPS];
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + BM * 4 + BN * 4 + 2 * LIC_MAX_TAPS];
   int* rowpix = (int*)(smem + 2 * BUF);
-  int8_t* tdy = (int8_t*)(smem + 2 * BUF + BM * 4);
+  float* sbias = (float*)(rowpix + BM);
+  int8_t* tdy = (int8_t*)(sbias + BN);
   int8_t* tdx = tdy + LIC_MAX_TAPS;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -43,6 +45,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
   const int mij = a.mi * a.mj;
 
   if (tid < a.ntaps) { tdy[tid] = a.dy[tid]; tdx[tid] = a.dx[tid]; }
+  for (int n = tid; n < BN; n += NT) sbias[n] = (a.bias && n0 + n < a.co) ? a.bias[n0 + n] : 0.f;
 
   // A-row decode (each thread loads chunk (tid&3) of rows (tid>>2) + r*NT/4)
   const int chunk = tid & 3;
@@ -201,9 +204,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
   // activation, residual / gate / GDN / half-tanh, channel-offset + shuffle
   // addressing, contiguous stores.
   float* ct = (float*)smem + wave * (32 * 33);
-  const bool vec_ok = epi_vec_ok<T>(a);
-#pragma nounroll
-  for (int q = 0; q < TM * TN; ++q) {
+  epilogue_all<T, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, [&](int q) {
+    // the accumulator is read only through compile-time indices
 #pragma unroll
     for (int qq = 0; qq < TM * TN; ++qq)
       if (qq == q) {
@@ -211,10 +213,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
         for (int r = 0; r < 16; ++r)
           ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r];
       }
-    __syncthreads();
-    epilogue_tile<T>(a, ct, rowpix + wm * WTM + (q / TN) * 32, n0 + wn * WTN + (q % TN) * 32, lane, vec_ok);
-    __syncthreads();
-  }
+  });
 }
 
 // Direct (VALU) convolution for tiny / misaligned channel counts (Cin = 1 or 3,

@@ -16,6 +16,27 @@
 // v_mfma_f32_32x32x2_f32 x4 (exact fp32).  Epilogue as conv.hip (LDS-staged).
 #include "lic_common.h"
 
+// diagnostic ablations (-DHALO_ABL=bits, timing only; outputs are wrong):
+//   1 no in-loop loads, 2 no epilogue, 4 no weight loads, 8 no halo loads
+#ifndef HALO_ABL
+#define HALO_ABL 0
+#endif
+#ifndef HALO_STAMP
+#define HALO_STAMP 0
+#endif
+// diagnostic build only (-DHALO_STAMP=1, tools/halo_stamps.py): per-phase s_memtime
+// sums per block, written past the end of the output (the caller allocates room)
+#if HALO_STAMP
+#define HSTAMP(v)                                                                        \
+  do {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+  } while (0)
+#else
+#define HSTAMP(v)
+#endif
+
 namespace lic {
 
 __device__ __attribute__((aligned(256))) unsigned char g_lic_zero_page[256];
@@ -27,7 +48,10 @@ struct HaloPlan {
   int ngroups;
   int tiles_y, tiles_x;
   int smem;        // dynamic LDS bytes
-  int16_t toff[LIC_MAX_TAPS];  // (dy - dymin) * hw + (dx - dxmin)
+  int rp_off;      // byte offset of rowpix[BM] + bias[BN] (past the epilogue slots)
+  // taps form a grid in tap order: tap t sits at halo offset
+  //   toff0 + (t / nx) * ystep + (t % nx) * xstep   (computed in scalar registers)
+  int toff0, nx, ystep, xstep;
   int dymin, dxmin;
 };
 
@@ -52,8 +76,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
   const int wbytes = p.G * BN * 32;
   char* hbuf0 = smem;
   char* wbuf0 = smem + 2 * hbytes;
-  int* rowpix = (int*)(wbuf0 + 2 * wbytes);
-  int16_t* stoff = (int16_t*)(rowpix + BM);
+  int* rowpix = (int*)(smem + p.rp_off);
+  float* sbias = (float*)(rowpix + BM);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -68,7 +92,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
   const int i0 = ty_t * TH, j0 = tx_t * TW;
   const int iy0 = i0 * a.isy + p.dymin, ix0 = j0 * a.isx + p.dxmin;
 
-  for (int t = tid; t < a.ntaps; t += NT) stoff[t] = p.toff[t];
+  for (int n = tid; n < BN; n += NT) sbias[n] = (a.bias && n0 + n < a.co) ? a.bias[n0 + n] : 0.f;
   for (int m = tid; m < BM; m += NT) {
     const int i = i0 + m / TW, j = j0 + m % TW;
     int base = -1;
@@ -137,24 +161,46 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
 #pragma unroll
       for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
 
+#if HALO_STAMP
+  unsigned long long st_begin = 0, st_loop = 0, st_a = 0, st_b = 0, st_c = 0, st_end = 0, rt_begin = 0, rt_end = 0;
+  unsigned long long sum_issue = 0, sum_comp = 0, sum_wait = 0;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt_begin)::"memory");
+#endif
+  HSTAMP(st_begin);
   if (nst > 0) {
     issue_halo(0, 0);
     issue_w(0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  HSTAMP(st_loop);
 
   for (int s = 0; s < nst; ++s) {
     const int k = s / p.ngroups, g = s - k * p.ngroups;
+    HSTAMP(st_a);
+#if !(HALO_ABL & 1)
+#if !(HALO_ABL & 4)
     if (s + 1 < nst) issue_w(s + 1, (s + 1) & 1);
+#endif
+#if !(HALO_ABL & 8)
     if (g == 0 && k + 1 < nchunks) issue_halo(k + 1, (k + 1) & 1);
+#endif
+#endif
+    HSTAMP(st_b);
     const char* hb = hbuf0 + (k & 1) * hbytes;
     const char* wb = wbuf0 + (s & 1) * wbytes;
     const int t0 = g * p.G;
     const int gcur = min(p.G, a.ntaps - t0);
-    for (int tt = 0; tt < gcur; ++tt) {
-      const int toff = stoff[t0 + tt];
-      u32x4 fa[TM], fb[TN];
+    // fragments of tap tt+1 are read while tap tt's MFMAs run (two register sets);
+    // the tap offset is a scalar grid cursor (no memory access inside the loop:
+    // an SMEM load would force lgkmcnt(0) and drain the in-flight LDS reads)
+    int cy = t0 / p.nx, cx = t0 - cy * p.nx;
+    auto load_frags = [&](int tt, u32x4(&fa)[TM], u32x4(&fb)[TN]) {
+      const int toff = p.toff0 + cy * p.ystep + cx * p.xstep;
+      if (++cx == p.nx) {
+        cx = 0;
+        ++cy;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int hp = hbase[i] + toff;
@@ -165,12 +211,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
         const int n = wn * WTN + j * 32 + lrow;
         fb[j] = *(const u32x4*)(wb + (tt * BN + n) * 32 + ((lhalf ^ ((n >> 3) & 1)) << 4));
       }
+    };
+    auto mfmas = [&](const u32x4(&fa)[TM], const u32x4(&fb)[TN]) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (sizeof(T) == 2) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(half8*)&fa[i], *(half8*)&fb[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&fa[i], *(const half8*)&fb[j],
+                                                               acc[i][j], 0, 0, 0);
           } else {
             const float* af = (const float*)&fa[i];
             const float* bf = (const float*)&fb[j];
@@ -179,18 +228,48 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q], bf[q], acc[i][j], 0, 0, 0);
           }
         }
+    };
+    u32x4 fa[2][TM], fb[2][TN];
+    load_frags(0, fa[0], fb[0]);
+    int tt = 0;
+    for (; tt + 2 <= gcur; tt += 2) {
+      load_frags(tt + 1, fa[1], fb[1]);
+      mfmas(fa[0], fb[0]);
+      // unconditional (a read past the group's last tap stays inside the LDS
+      // allocation and is discarded)
+      load_frags(tt + 2, fa[0], fb[0]);
+      mfmas(fa[1], fb[1]);
     }
+    if (tt < gcur) mfmas(fa[0], fb[0]);
+    HSTAMP(st_c);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#if HALO_STAMP
+    unsigned long long st_d;
+    HSTAMP(st_d);
+    sum_issue += st_b - st_a;
+    sum_comp += st_c - st_b;
+    sum_wait += st_d - st_c;
+#endif
   }
 
+#if HALO_ABL & 2
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z += acc[i][j][r];
+    if (z == 1234.5f) ((float*)a.y)[tid] = z;
+    return;
+  }
+#endif
   // epilogue (LDS-staged, one 32x32 tile per wave at a time; see conv.hip)
   float* ct = (float*)smem + wave * (32 * 33);
-  const bool vec_ok = epi_vec_ok<T>(a);
-  // runtime loop over tiles (the epilogue body is emitted once); the accumulator
-  // is read only through the compile-time-indexed selector below
-#pragma nounroll
-  for (int q = 0; q < TM * TN; ++q) {
+  epilogue_all<T, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, [&](int q) {
+    // the accumulator is read only through compile-time indices
 #pragma unroll
     for (int qq = 0; qq < TM * TN; ++qq)
       if (qq == q) {
@@ -198,10 +277,23 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
         for (int r = 0; r < 16; ++r)
           ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r];
       }
-    __syncthreads();
-    epilogue_tile<T>(a, ct, rowpix + wm * WTM + (q / TN) * 32, n0 + wn * WTN + (q % TN) * 32, lane, vec_ok);
-    __syncthreads();
+  });
+#if HALO_STAMP
+  HSTAMP(st_end);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt_end)::"memory");
+  if (tid == 0) {
+    unsigned long long* o = (unsigned long long*)((T*)a.y + (size_t)a.n * a.ho * a.wo * a.ldy) +
+                             ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+    o[0] = st_loop - st_begin;
+    o[1] = sum_issue;
+    o[2] = sum_comp;
+    o[3] = sum_wait;
+    o[4] = st_end - st_loop - sum_issue - sum_comp - sum_wait;
+    o[5] = rt_begin;
+    o[6] = rt_end;
+    o[7] = __smid();
   }
+#endif
 }
 
 // Returns 1 and launches when the halo kernel applies; 0 to let the caller fall back.
@@ -228,7 +320,7 @@ static int try_halo(const lic_conv_args& a, hipStream_t s, int& status) {
   if (hpix > 32767) return 0;
   p.hpix_pad = (hpix + 31) / 32 * 32;
   const int hbytes = p.hpix_pad * 32;
-  const int budget = 160 * 1024 - 2 * hbytes - (TH * TW * 4) - 2 * LIC_MAX_TAPS - 64;
+  const int budget = 160 * 1024 - 2 * hbytes - (TH * TW * 4) - BN * 4;
   int G = budget / (2 * BN * 32);
   if (G < 1) return 0;
   if (G > a.ntaps) G = a.ntaps;
@@ -236,10 +328,24 @@ static int try_halo(const lic_conv_args& a, hipStream_t s, int& status) {
   p.ngroups = (a.ntaps + G - 1) / G;
   p.tiles_y = (a.mi + TH - 1) / TH;
   p.tiles_x = (a.mj + TW - 1) / TW;
-  for (int t = 0; t < a.ntaps; ++t) p.toff[t] = (int16_t)((a.dy[t] - dymin) * p.hw + (a.dx[t] - dxmin));
-  int smem = 2 * hbytes + 2 * G * BN * 32 + TH * TW * 4 + 2 * LIC_MAX_TAPS;
+  // tap grid: row length nx = taps sharing the first tap's dy; every tap t must
+  // sit at (dy0 + (t/nx)*sy, dx0 + (t%nx)*sx) (kxk convs and the transposed-conv
+  // phases of functional.pack_conv_transpose2d all do)
+  int nx = 1;
+  while (nx < a.ntaps && a.dy[nx] == a.dy[0]) ++nx;
+  if (a.ntaps % nx) return 0;
+  const int sy = a.ntaps > nx ? a.dy[nx] - a.dy[0] : 0;
+  const int sx = nx > 1 ? a.dx[1] - a.dx[0] : 0;
+  for (int t = 0; t < a.ntaps; ++t)
+    if (a.dy[t] != a.dy[0] + (t / nx) * sy || a.dx[t] != a.dx[0] + (t % nx) * sx) return 0;
+  p.toff0 = (a.dy[0] - dymin) * p.hw + (a.dx[0] - dxmin);
+  p.nx = nx;
+  p.ystep = sy * p.hw;
+  p.xstep = sx;
   const int epi_bytes = (NT / 64) * 32 * 33 * 4;
-  if (smem < epi_bytes) smem = epi_bytes;
+  p.rp_off = 2 * hbytes + 2 * G * BN * 32;
+  if (p.rp_off < epi_bytes) p.rp_off = epi_bytes;
+  const int smem = p.rp_off + TH * TW * 4 + BN * 4;
   p.smem = smem;
   if (smem > 160 * 1024) return 0;
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;

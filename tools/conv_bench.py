@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--dtype", default="fp16")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated shape names")
+    ap.add_argument("--auto-only", action="store_true")
     args = ap.parse_args()
     import lic_amd.functional as Fn
     from lic_amd.layers import Conv2d
@@ -39,6 +41,8 @@ def main():
     dev = "cuda"
     st = torch.cuda.current_stream()
     for name, ci, co, k, s, pad, H in SHAPES:
+        if args.only and name not in args.only.split(","):
+            continue
         m = Conv2d(ci, co, k, s, 0).to(dev)
         x = Fn.Act(torch.randn(args.batch, H, H, ci, device=dev).to(dt))
         pk = m.packed(dt, pad)
@@ -46,7 +50,7 @@ def main():
         out = Fn.Act.empty(args.batch, Ho, Wo, co, dt, dev)
         flops = 2.0 * args.batch * Ho * Wo * co * ci * k * k
         res = {}
-        for variant in ("auto", "generic", "auto", "generic"):
+        for variant in (("auto",) * 3 if args.auto_only else ("auto", "generic", "auto", "generic")):
             kw = dict(force_generic=(variant == "generic"))
             for _ in range(2):
                 Fn.conv(x, pk, out, **kw)
