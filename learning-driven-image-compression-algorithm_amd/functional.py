@@ -35,6 +35,14 @@ def _lib():
     return _ffi.load()
 
 
+def _dp(t: torch.Tensor) -> int:
+    """Device pointer of a GPU tensor; host tensors are refused (the kernels would
+    dereference a host address)."""
+    if not t.is_cuda:
+        raise ValueError("liblic: tensor is not on the GPU (move the module / inputs to 'cuda')")
+    return t.data_ptr()
+
+
 class Act:
     """NHWC activation view: channels [c0, c0 + c) of a contiguous [B, H, W, Ctot] tensor.
     ``zpad`` >= c: channels [c0 + c, c0 + zpad) are known to be zero (lets a Cin=3 layer
@@ -71,7 +79,7 @@ class Act:
 
     @property
     def ptr(self):
-        return self.t.data_ptr() + self.c0 * self.t.element_size()
+        return _dp(self.t) + self.c0 * self.t.element_size()
 
     @property
     def dtype(self):
@@ -103,7 +111,7 @@ class Act:
             epc = 16 // torch.empty((), dtype=dtype).element_size()
             cp = -(-C // epc) * epc if pad16 else C
             out = Act(torch.empty((B, H, W, cp), dtype=dtype, device=x.device), 0, C, cp)
-            check(_lib().lic_nchw_to_nhwc(dtype_id(dtype), x.data_ptr(), B, C, H, W, out.ptr, out.ld, cp,
+            check(_lib().lic_nchw_to_nhwc(dtype_id(dtype), _dp(x), B, C, H, W, out.ptr, out.ld, cp,
                                           stream_handle()))
             return out
         return Act(t.to(dtype).contiguous())
@@ -252,8 +260,8 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
         a.dy[t] = pk.dy[t]
         a.dx[t] = pk.dx[t]
     a.groups = pk.groups
-    a.wgt, a.cpad, a.copad = pk.w.data_ptr(), pk.cpad, pk.copad
-    a.bias = pk.bias.data_ptr() if pk.bias is not None else None
+    a.wgt, a.cpad, a.copad = _dp(pk.w), pk.cpad, pk.copad
+    a.bias = _dp(pk.bias) if pk.bias is not None else None
     a.prologue, a.act, a.slope, a.epi = prologue, act, slope, epi
     a.r1, a.ldr1 = _ptr(r1)
     a.g, a.ldg = _ptr(g)
@@ -281,9 +289,9 @@ def gdn_prepare(beta: torch.Tensor, gamma: torch.Tensor, beta_bound: float, gamm
     copad = _choose_copad(C)
     w = torch.empty((copad, 1, cpad), dtype=dtype, device=beta.device)
     b = torch.empty((C,), dtype=torch.float32, device=beta.device)
-    check(_lib().lic_gdn_prepare(dtype_id(dtype), beta.detach().float().contiguous().data_ptr(),
-                                 gamma.detach().float().contiguous().data_ptr(), C, beta_bound, gamma_bound,
-                                 pedestal, w.data_ptr(), cpad, copad, b.data_ptr(), stream_handle()))
+    check(_lib().lic_gdn_prepare(dtype_id(dtype), _dp(beta.detach().float().contiguous()),
+                                 _dp(gamma.detach().float().contiguous()), C, beta_bound, gamma_bound,
+                                 pedestal, _dp(w), cpad, copad, _dp(b), stream_handle()))
     return ConvPack(w=w, bias=b, ci=C, co=C, dy=[0], dx=[0])
 
 
@@ -302,7 +310,7 @@ def win_attn(qkv: Act, C: int, heads: int, ws: int, shift: int, table: torch.Ten
     a.qkv, a.n, a.h, a.w, a.c, a.ldqkv = qkv.ptr, qkv.B, qkv.H, qkv.W, C, qkv.ld
     a.out, a.ldo = out.ptr, out.ld
     a.heads, a.ws, a.shift = heads, ws, shift
-    a.table, a.tab_sr, a.tab_sh = table.data_ptr(), tab_sr, tab_sh
+    a.table, a.tab_sr, a.tab_sh = _dp(table), tab_sr, tab_sh
     a.mask_kind, a.scale_after, a.scale = mask_kind, 1 if scale_after else 0, scale
     a.force_valu = 1 if force_valu else 0
     check(_lib().lic_win_attn_fwd(ctypes.byref(a), stream_handle()))
@@ -312,7 +320,7 @@ def win_attn(qkv: Act, C: int, heads: int, ws: int, shift: int, table: torch.Ten
 def layernorm(x: Act, weight: torch.Tensor, bias: torch.Tensor, eps: float, out: Optional[Act] = None) -> Act:
     if out is None:
         out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)
-    check(_lib().lic_layernorm_fwd(dtype_id(x.dtype), x.ptr, x.npix, x.c, x.ld, weight.data_ptr(), bias.data_ptr(),
+    check(_lib().lic_layernorm_fwd(dtype_id(x.dtype), x.ptr, x.npix, x.c, x.ld, _dp(weight), _dp(bias),
                                    eps, out.ptr, out.ld, stream_handle()))
     return out
 
@@ -324,7 +332,7 @@ def rb3(x: Act, params: torch.Tensor, out: Optional[Act] = None) -> Act:
     if out is None:
         epc = 16 // x.t.element_size()
         out = Act(torch.empty((x.B, x.H, x.W, epc), dtype=x.dtype, device=x.t.device), 0, 3, epc)
-    check(_lib().lic_rb3_fwd(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.ld, params.data_ptr(), out.ptr, out.ld,
+    check(_lib().lic_rb3_fwd(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.ld, _dp(params), out.ptr, out.ld,
                              stream_handle()))
     return out
 
@@ -353,7 +361,7 @@ def quantize_median(z: Act, medians: Optional[torch.Tensor], out: Optional[Act] 
     if out is None:
         out = Act.empty(z.B, z.H, z.W, z.c, z.dtype, z.t.device)
     check(_lib().lic_quantize_median(dtype_id(z.dtype), z.ptr, z.npix, z.c, z.ld,
-                                     medians.data_ptr() if medians is not None else None,
+                                     _dp(medians) if medians is not None else None,
                                      out.ptr, out.ld, stream_handle()))
     return out
 
@@ -375,7 +383,7 @@ def gauss_rate(y: Act, mu: Act, scale: Act, partials: torch.Tensor, part_off: in
     n = -(-(y.npix * y.c) // 256)
     if part_off + n > partials.numel():
         raise ValueError("gauss_rate: partials buffer too small")
-    a.partials = partials.data_ptr() + part_off * 8
+    a.partials = _dp(partials) + part_off * 8
     a.max_parts = partials.numel() - part_off
     a.scale_bound, a.likelihood_bound = scale_bound, likelihood_bound
     check(_lib().lic_gauss_rate_fwd(ctypes.byref(a), stream_handle()))
@@ -384,26 +392,26 @@ def gauss_rate(y: Act, mu: Act, scale: Act, partials: torch.Tensor, part_off: in
 
 def bpp_finalize(partials: torch.Tensor, nparts: int, num_pixels: float, out: torch.Tensor,
                  sum_out: Optional[torch.Tensor] = None):
-    check(_lib().lic_bpp_finalize(partials.data_ptr(), nparts, float(num_pixels), out.data_ptr(),
-                                  sum_out.data_ptr() if sum_out is not None else None, stream_handle()))
+    check(_lib().lic_bpp_finalize(_dp(partials), nparts, float(num_pixels), _dp(out),
+                                  _dp(sum_out) if sum_out is not None else None, stream_handle()))
 
 
 def syntax_recon(xtil: Act, wgen: Act, x: torch.Tensor, x_rec: torch.Tensor, parts: torch.Tensor,
                  parts_per_img: int):
     B, _, H, W = x.shape
     check(_lib().lic_syntax_recon_fwd(dtype_id(xtil.dtype), xtil.ptr, B, H, W, xtil.c, xtil.ld, wgen.ptr, wgen.ld,
-                                      x.data_ptr(), x_rec.data_ptr(), parts.data_ptr(), parts_per_img,
+                                      _dp(x), _dp(x_rec), _dp(parts), parts_per_img,
                                       stream_handle()))
 
 
 def psnr_finalize(parts: torch.Tensor, B: int, parts_per_img: int, count: float, v_mse: torch.Tensor,
                   v_psnr: torch.Tensor):
-    check(_lib().lic_psnr_finalize(parts.data_ptr(), B, parts_per_img, float(count), v_mse.data_ptr(),
-                                   v_psnr.data_ptr(), stream_handle()))
+    check(_lib().lic_psnr_finalize(_dp(parts), B, parts_per_img, float(count), _dp(v_mse),
+                                   _dp(v_psnr), stream_handle()))
 
 
 def to_nchw_f32(x: Act) -> torch.Tensor:
     out = torch.empty((x.B, x.c, x.H, x.W), dtype=torch.float32, device=x.t.device)
-    check(_lib().lic_nhwc_to_nchw(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.c, x.ld, out.data_ptr(),
+    check(_lib().lic_nhwc_to_nchw(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.c, x.ld, _dp(out),
                                   stream_handle()))
     return out

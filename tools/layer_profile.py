@@ -1,0 +1,86 @@
+"""Per-op GPU time of one Net.forward (eager, each op synchronised and timed with
+HIP events), aggregated by calling module and op shape.
+
+usage: python tools/layer_profile.py [--arch net_ga] [--batch 32] [--size 256] [--top 40]
+Timings are serialised (no stream overlap), so their sum exceeds the graph-replay
+step time; use them to rank ops, not to predict the step.
+"""
+import argparse
+import collections
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import lic_amd.functional as Fn  # noqa: E402
+
+REC = collections.defaultdict(lambda: [0, 0.0])
+
+
+def _label(name, args):
+    site = "?"
+    fr = sys._getframe(2)
+    for _ in range(8):
+        if fr is None:
+            break
+        slf = fr.f_locals.get("self")
+        if slf is not None and isinstance(slf, torch.nn.Module):
+            site = f"{type(slf).__name__}.{fr.f_code.co_name}"
+            break
+        fr = fr.f_back
+    shape = ""
+    x = args[0] if args else None
+    if isinstance(x, Fn.Act):
+        shape = f"{x.H}x{x.W}x{x.c}"
+    if name in ("conv", "conv_transpose") and len(args) > 1:
+        pk = args[1][0] if isinstance(args[1], (list, tuple)) else args[1]
+        shape += f" {pk.ci}->{pk.co} k{pk.kh}s{pk.stride}"
+    return f"{name:14s} {site:40s} {shape}"
+
+
+def wrap(name):
+    fn = getattr(Fn, name)
+
+    def w(*args, **kw):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn(*args, **kw)
+        e1.record()
+        e1.synchronize()
+        r = REC[_label(name, args)]
+        r[0] += 1
+        r[1] += e0.elapsed_time(e1)
+        return out
+    setattr(Fn, name, w)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arch", default="net_ga")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--top", type=int, default=45)
+    args = ap.parse_args()
+    import bench
+    net = bench.build_net(args.arch, "fp16", args.size, args.batch, "cpu").to("cuda")
+    x = torch.rand(args.batch, 3, args.size, args.size, device="cuda") * 2 - 1
+    with torch.no_grad():
+        print("warm-up forward", flush=True)
+        net(x, "test")
+        torch.cuda.synchronize()
+        print("profiled forward", flush=True)
+        for n in ("conv", "conv_transpose", "gdn", "win_attn", "layernorm", "rb3", "add", "copy", "avgpool",
+                  "quantize_median", "gauss_rate", "syntax_recon", "bpp_finalize", "psnr_finalize"):
+            wrap(n)
+        net(x, "test")
+        torch.cuda.synchronize()
+    tot = sum(v[1] for v in REC.values())
+    print(f"# serialised op time {tot:.3f} ms over {sum(v[0] for v in REC.values())} ops")
+    for k, (n, t) in sorted(REC.items(), key=lambda kv: -kv[1][1])[:args.top]:
+        print(f"{t:8.3f} ms {100 * t / tot:5.1f}% x{n:<4d} {k}")
+
+
+if __name__ == "__main__":
+    main()
