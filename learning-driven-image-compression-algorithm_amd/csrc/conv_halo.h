@@ -14,6 +14,7 @@
 // fragment reads of 16 consecutive pixels / channels are conflict-free.
 // Fragments: f16 v_mfma_f32_32x32x16_f16 (one per tap and 32x32 tile); f32
 // v_mfma_f32_32x32x2_f32 x4 (exact fp32).  Epilogue as conv.hip (LDS-staged).
+#pragma once
 #include "lic_common.h"
 
 // diagnostic ablations (-DHALO_ABL=bits, timing only; outputs are wrong):
@@ -39,7 +40,7 @@
 
 namespace lic {
 
-__device__ __attribute__((aligned(256))) unsigned char g_lic_zero_page[256];
+static __device__ __attribute__((aligned(256))) unsigned char g_lic_zero_page[256];
 
 struct HaloPlan {
   int hh, hw;      // halo rows / cols
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
 
 // Returns 1 and launches when the halo kernel applies; 0 to let the caller fall back.
 template <typename T, int TH, int TW, int BN, int WM, int WN>
-static int try_halo(const lic_conv_args& a, hipStream_t s, int& status) {
+int try_halo(const lic_conv_args& a, hipStream_t s, int& status) {
   constexpr int E = 16 / (int)sizeof(T);
   constexpr int CK = 2 * E;
   constexpr int NT = WM * WN * 64;
@@ -376,8 +377,5 @@ int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   }
   return 0;
 }
-
-template int conv_halo_dispatch<float>(const lic_conv_args&, hipStream_t, int&);
-template int conv_halo_dispatch<half_t>(const lic_conv_args&, hipStream_t, int&);
 
 }  // namespace lic

@@ -1,16 +1,16 @@
 #!/bin/bash
-# Build liblic variants of conv_halo.hip into ab/ for A/B timing.
+# Build liblic variants of the f16 halo conv (conv_halo_f16.hip) into ab/ for A/B timing.
 # usage: tools/build_ab.sh name:"-DFLAG=.. -DFLAG2=.." ...
 set -e
 cd "$(dirname "$0")/../learning-driven-image-compression-algorithm_amd/csrc"
 make -s
 mkdir -p ../../ab
-OBJS=$(ls build/*.o | grep -v conv_halo)
+OBJS=$(ls build/*.o | grep -v conv_halo_f16)
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I."
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
-  (/opt/rocm/bin/hipcc $F $defs -c conv_halo.hip -o /tmp/ch_$name.o -Rpass-analysis=kernel-resource-usage 2>&1 \
-     | grep -E "VGPRs:|Scratch" | sed -n 5,6p | sed "s/^/$name /"
+  (/opt/rocm/bin/hipcc $F $defs -c conv_halo_f16.hip -o /tmp/ch_$name.o -Rpass-analysis=kernel-resource-usage 2>&1 \
+     | grep -E "VGPRs:|Scratch" | sed -n 1,2p | sed "s/^/$name /"
    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS /tmp/ch_$name.o -o ../../ab/liblic_$name.so) &
 done
 wait
