@@ -57,10 +57,19 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
   const T* qkv = (const T*)a.qkv;
   const int64_t ldq = a.ldqkv;
   const int qoff = hc * d, koff = a.c + hc * d, voff = 2 * a.c + hc * d;
-  // V^T staging: lane t writes V[t][0..31] (zeros beyond d) into vT[c][t]
+  // V^T staging: lane t loads its V row with 16-byte loads (d % (16 / sizeof(T)) == 0)
+  // and scatters it transposed into vT[c][t] (zeros for c >= d)
   {
+    constexpr int VE = 16 / (int)sizeof(T);
     const T* vp = qkv + (int64_t)pixs[lane] * ldq + voff;
-    for (int c = 0; c < 32; ++c) vT[wave][c * VT_LD + lane] = c < d ? vp[c] : from_f<T>(0.f);
+#pragma unroll
+    for (int c0 = 0; c0 < 32; c0 += VE) {
+      u32x4 raw = {0u, 0u, 0u, 0u};
+      if (c0 < d) raw = *(const u32x4*)(vp + c0);
+      const T* e = (const T*)&raw;
+#pragma unroll
+      for (int k = 0; k < VE; ++k) vT[wave][(c0 + k) * VT_LD + lane] = e[k];
+    }
   }
   __syncthreads();
 
@@ -218,7 +227,7 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
 int win_attn_mfma_dispatch(const lic_attn_args& a, hipStream_t s, int& status) {
   const int d = a.c / a.heads;
   if (a.ws != 8 || d > 32 || d % 8 || a.ldqkv % 8 || a.force_valu) return 0;
-  if (a.dtype == LIC_F16 && ((uintptr_t)a.qkv % 16)) return 0;
+  if ((uintptr_t)a.qkv % 16) return 0;
   const int64_t blocks = (int64_t)a.n * (a.h / 8) * (a.w / 8) * ((a.heads + 3) / 4);
   if (a.dtype == LIC_F16)
     hipLaunchKernelGGL(win_attn_mfma_kernel<half_t>, dim3((unsigned)blocks), dim3(256), 0, s, a);

@@ -10,6 +10,33 @@ namespace lic {
 template <typename T, int BM, int BN, int WM, int WN>
 int launch_mfma(const lic_conv_args& a, int M, hipStream_t s);
 
+// Spatial-tile ("halo") launches, instantiated in conv_halo_*.hip.  Return 1 and
+// launch when the tile config applies, 0 to fall back.
+template <typename T, int TH, int TW, int BN, int WM, int WN>
+int try_halo(const lic_conv_args& a, hipStream_t s, int& status);
+
+// Halo tile choice: the largest output-channel block whose grid still fills the
+// chip (>= 200 workgroups of 16x16 pixels), then 8x8-pixel tiles for small maps
+// (the 16x16 latents of the slice loop).
+template <typename T>
+static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
+  if (a.groups != 1 || a.ntaps < 2 || a.prologue != LIC_PRO_NONE || a.force_direct) return 0;
+  auto blocks = [&](int th, int tw, int bn) {
+    return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
+  };
+  // 16x16 tiles only where at most half of a tile row / column can fall off the map
+  const bool big_map = a.mi > 8 && a.mj > 8;
+  if (big_map) {
+    if (a.copad % 192 == 0 && blocks(16, 16, 192) >= 200) return try_halo<T, 16, 16, 192, 4, 2>(a, s, status);
+    if (a.copad % 128 == 0 && blocks(16, 16, 128) >= 200) return try_halo<T, 16, 16, 128, 4, 2>(a, s, status);
+    if (a.copad % 64 == 0 && blocks(16, 16, 64) >= 200) return try_halo<T, 16, 16, 64, 4, 2>(a, s, status);
+    if (a.copad % 32 == 0 && blocks(16, 16, 32) >= 200) return try_halo<T, 16, 16, 32, 8, 1>(a, s, status);
+  }
+  if (a.copad % 64 == 0 && blocks(8, 8, 64) >= 128) return try_halo<T, 8, 8, 64, 2, 2>(a, s, status);
+  if (a.copad % 32 == 0 && blocks(8, 8, 32) >= 64) return try_halo<T, 8, 8, 32, 2, 1>(a, s, status);
+  return 0;
+}
+
 // Direct (VALU) convolution for tiny / misaligned channel counts (Cin = 1 or 3,
 // grouped / depthwise, 1x1 layers on a handful of pixels).  One thread computes
 // COG consecutive output channels of one pixel; the packed weights are staged in

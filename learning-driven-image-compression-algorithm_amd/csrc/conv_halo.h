@@ -363,19 +363,4 @@ int try_halo(const lic_conv_args& a, hipStream_t s, int& status) {
   return 1;
 }
 
-template <typename T>
-int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
-  if (a.groups != 1 || a.ntaps < 2 || a.prologue != LIC_PRO_NONE || a.force_direct) return 0;
-  const int64_t tiles16 = (int64_t)a.n * ((a.mi + 15) / 16) * ((a.mj + 15) / 16);
-  if (a.copad % 192 == 0) {
-    if (tiles16 * (a.copad / 192) < 200) return 0;
-    return try_halo<T, 16, 16, 192, 4, 2>(a, s, status);
-  }
-  if (a.copad % 128 == 0) {
-    if (tiles16 * (a.copad / 128) < 200) return 0;
-    return try_halo<T, 16, 16, 128, 4, 2>(a, s, status);
-  }
-  return 0;
-}
-
 }  // namespace lic

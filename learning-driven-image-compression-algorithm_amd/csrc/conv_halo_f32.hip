@@ -1,8 +1,9 @@
-// Instantiation of the halo conv (conv_halo.h) for f32.
+// Instantiations of the halo conv (conv_halo.h) for f32: large tiles.
 #include "conv_halo.h"
 
 namespace lic {
 
-template int conv_halo_dispatch<float>(const lic_conv_args&, hipStream_t, int&);
+template int try_halo<float, 16, 16, 192, 4, 2>(const lic_conv_args&, hipStream_t, int&);
+template int try_halo<float, 16, 16, 128, 4, 2>(const lic_conv_args&, hipStream_t, int&);
 
 }  // namespace lic

@@ -404,7 +404,4 @@ __device__ __forceinline__ void epilogue_all(const lic_conv_args& a, const float
   }
 }
 
-template <typename T>
-int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
-
 }  // namespace lic
