@@ -123,43 +123,59 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
     }
   }
 
-  // scale + bias + mask + softmax over keys (rows) for each query (lane column)
+  // scale + bias + mask + softmax over keys (rows) for each query (lane column).
+  // Register r of key tile tj holds key j = 32tj + 8(r>>2) + 4h + (r&3), i.e. key row
+  // 4tj + (r>>2), column 4h + (r&3): the bias index (iy-jy+7)*15 + (ix-jx+7) is a
+  // per-lane base minus a compile-time offset.  Masks can only differ from zero in
+  // the last window row / column (uniform branch).
   const int split = ws - a.shift;
   const bool last_row = wy == nwy - 1, last_col = wx == nwx - 1;
+  const bool mask_on = a.mask_kind != 0 && (last_row || last_col);
   auto reg_wba = [&](int y, int x) {
     const int ly = y < a.h - ws ? 0 : (y < a.h - a.shift ? 1 : 2);
     const int lx = x < a.w - ws ? 0 : (x < a.w - a.shift ? 1 : 2);
     return ly * 3 + lx;
   };
+  constexpr float L2E = 1.4426950408889634f;
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti) {
     const int i = 32 * ti + lr;
     const int iy = i / ws, ix = i % ws;
-    const int my_reg = a.mask_kind == 1 ? reg_wba(wy * ws + iy, wx * ws + ix) : 0;
+    const float* trow = &tab[wave][(iy + ws - 1) * (2 * ws - 1) + (ix + ws - 1) - 4 * lh];
     float mx = -INFINITY;
 #pragma unroll
     for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int j = 32 * tj + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const int jy = j / ws, jx = j % ws;
-        float v = S[tj][ti][r] * scale + tab[wave][(iy - jy + ws - 1) * (2 * ws - 1) + (ix - jx + ws - 1)];
-        if (a.mask_kind == 1) {
-          if (reg_wba(wy * ws + jy, wx * ws + jx) != my_reg) v += -100.0f;
-        } else if (a.mask_kind == 2) {
-          if ((last_row && ((iy < split) != (jy < split))) || (last_col && ((ix < split) != (jx < split))))
-            v = -INFINITY;
-        }
+        const float v = S[tj][ti][r] * scale + trow[-((4 * tj + (r >> 2)) * (2 * ws - 1) + (r & 3))];
         S[tj][ti][r] = v;
-        mx = fmaxf(mx, v);
       }
+    if (mask_on) {
+      const int my_reg = a.mask_kind == 1 ? reg_wba(wy * ws + iy, wx * ws + ix) : 0;
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int jy = 4 * tj + (r >> 2), jx = 4 * lh + (r & 3);
+          if (a.mask_kind == 1) {
+            if (reg_wba(wy * ws + jy, wx * ws + jx) != my_reg) S[tj][ti][r] += -100.0f;
+          } else if ((last_row && ((iy < split) != (jy < split))) || (last_col && ((ix < split) != (jx < split)))) {
+            S[tj][ti][r] = -INFINITY;
+          }
+        }
+    }
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[tj][ti][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mxl = mx * L2E;
     float sum = 0.f;
 #pragma unroll
     for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e = expf(S[tj][ti][r] - mx);
+        const float e = __builtin_amdgcn_exp2f(fmaf(S[tj][ti][r], L2E, -mxl));
         S[tj][ti][r] = e;
         sum += e;
       }
