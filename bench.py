@@ -23,7 +23,6 @@ import sys
 import time
 
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -145,11 +144,8 @@ def main():
                     help="only warm-up + timed replays (for rocprofv3 per-forward kernel breakdowns)")
     args = ap.parse_args()
 
-    world = _env_int("WORLD_SIZE", 1)
-    rank = _env_int("RANK", 0)
-    local = _env_int("LOCAL_RANK", 0)
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+    from lic_amd import distributed as D
+    rank, world, local = D.init("nccl")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dtype = torch.float16 if args.precision == "fp16" else torch.float32
@@ -171,22 +167,16 @@ def main():
     torch.cuda.synchronize()
 
     def timed(k):
-        if world > 1:
-            dist.barrier()
+        D.barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(k):
             run()
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        D.barrier(world)
         return time.perf_counter() - t0
 
-    elapsed = timed(args.steps)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = D.max_over_ranks(timed(args.steps), world, device)
     images = args.batch * args.steps * world
     value = images / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -220,7 +210,7 @@ def main():
                        "parallelism": f"image-sharded x{world} (independent batches, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": None,
-                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} (conv_mfma_kernel 128x192), "
+                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} (conv_halo_kernel 16x16 px x 192 ch), "
                                    f"{flops / 1e9:.1f} GFLOP/launch, {tk * 1e6:.1f} us/launch"},
             "a_model": {"ms": round(ta * 1e3, 3), "tflops": round(a_tflops, 2),
                         "frac_of_peak": round(a_tflops / peak, 4),
@@ -240,9 +230,7 @@ def main():
                                   "ms_per_step": round(t32 * 1e3, 3),
                                   "parity": parity_check(args.arch, "fp32", args.size, device)}
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    D.finish(world)
 
 
 if __name__ == "__main__":

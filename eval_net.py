@@ -44,10 +44,18 @@ def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing,
         raise NotImplementedError("--pre_processing (online encoder finetune) needs the training path "
                                   "(SURVEY.md 8(f) rank 4)")
     from lic_amd.model import net_ga, net_unet_ha_hs
+    from lic_amd import distributed as D
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
+    # one process per GPU under torch.distributed.run: images round-robin over ranks,
+    # one all-reduce of the summary sums at the end
+    rank, world, local = D.init("nccl")
+    if world > 1:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
     images = list(sorted(glob.glob(data_path)))
     if not all_images:
         images = images[22:23]
+    images = D.shard(images, rank, world)
     list_eval_bpp = list_v_psnr = list_v_mse = 0.0
     cnt = 0
     sum_time = 0.0
@@ -74,9 +82,12 @@ def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing,
         print(end_time - begin_time, img_name, eval_bpp.mean().item(), v_psnr.mean().item(),
               (eval_bpp + lmbda * v_mse).cpu().item())
         cnt += 1
-    if cnt:
+    sum_time, list_eval_bpp, list_v_psnr, list_v_mse, cnt = D.sum_over_ranks(
+        [sum_time, list_eval_bpp, list_v_psnr, list_v_mse, cnt], world, device)
+    if cnt and rank == 0:
         print('[WITHOUT PRE-PROCESSING] ave_time:%.4f bpp: %.4f psnr: %.4f  v_mse: %.4f' % (
             sum_time / cnt, list_eval_bpp / cnt, list_v_psnr / cnt, list_v_mse / cnt))
+    D.finish(world)
 
 
 def main(argv=None):

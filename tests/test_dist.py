@@ -1,0 +1,65 @@
+"""The N>1 path on CPU: world_size-2 gloo process groups exercising the image
+sharding, the MAX step-time reduction of bench.py and the single summary
+all-reduce of eval_net.py (lic_amd.distributed)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from lic_amd import distributed as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    r, w, _ = D.init("gloo")
+    assert (r, w) == (rank, world)
+    images = [f"img{i:02d}.png" for i in range(7)]
+    mine = D.shard(images, r, w)
+    # per-image statistics as eval_net.val accumulates them (time, bpp, psnr, mse, count)
+    stats = [0.0, 0.0, 0.0, 0.0, 0.0]
+    for name in mine:
+        i = images.index(name)
+        stats = [stats[0] + 0.01 * i, stats[1] + 0.5 + i, stats[2] + 30.0 + 0.25 * i, stats[3] + 2.0 * i, stats[4] + 1]
+    total = D.sum_over_ranks(stats, w)
+    D.barrier(w)
+    tmax = D.max_over_ranks(1.5 + rank, w)
+    q.put((rank, mine, total, tmax))
+    D.finish(w)
+
+
+def test_world2_shard_reduce_gloo():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    shards = [o[1] for o in out]
+    images = [f"img{i:02d}.png" for i in range(7)]
+    assert sorted(shards[0] + shards[1]) == images and not set(shards[0]) & set(shards[1])
+    ref = [sum(0.01 * i for i in range(7)), sum(0.5 + i for i in range(7)), sum(30.0 + 0.25 * i for i in range(7)),
+           sum(2.0 * i for i in range(7)), 7.0]
+    for o in out:
+        assert o[2] == pytest.approx(ref, rel=1e-12)
+        assert o[3] == 2.5   # MAX over ranks of 1.5 + rank
+
+
+def test_single_process_is_identity():
+    assert D.shard([1, 2, 3], 0, 1) == [1, 2, 3]
+    assert D.sum_over_ranks([1.0, 2.0], 1) == [1.0, 2.0]
+    assert D.max_over_ranks(3.0, 1) == 3.0
