@@ -22,9 +22,6 @@
 #ifndef HALO_ABL
 #define HALO_ABL 0
 #endif
-#ifndef HALO_INTERLEAVE
-#define HALO_INTERLEAVE 0
-#endif
 #ifndef HALO_STAMP
 #define HALO_STAMP 0
 #endif
@@ -148,42 +145,6 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
     }
   };
 
-  // Piece-wise form of issue_w / issue_halo (HALO_INTERLEAVE): piece it of this
-  // wave's share of the next stage's LDS-DMA (weights first, then the halo) so the
-  // transfers can be spread between the MFMAs of the current stage.
-  auto w_pieces = [&](int s) {
-    const int g = s % p.ngroups;
-    const int total = min(p.G, a.ntaps - g * p.G) * BN * 2;
-    return total > wave * 64 ? (total - wave * 64 + NT - 1) / NT : 0;
-  };
-  const int h_pieces = hq_total > wave * 64 ? (hq_total - wave * 64 + NT - 1) / NT : 0;
-  auto issue_w_piece = [&](int s, int buf, int it) {
-    const int k = s / p.ngroups, g = s - k * p.ngroups;
-    const int c0 = k * CK;
-    const int t0 = g * p.G;
-    const int q0 = wave * 64 + it * NT;
-    const int q = q0 + lane;
-    const int tt = q / (BN * 2);
-    const int n = (q >> 1) - tt * BN;
-    const int c = (q & 1) ^ ((n >> 3) & 1);
-    const T* src = wg + ((int64_t)(n0 + n) * a.ntaps + t0 + tt) * a.cpad + c0 + c * E;
-    glds16(src, wbuf0 + buf * wbytes + q0 * 16);
-  };
-  auto issue_h_piece = [&](int k, int buf, int it) {
-    const int c0 = k * CK;
-    const int q0 = wave * 64 + it * NT;
-    const int q = q0 + lane;
-    const int hp = q >> 1;
-    const int c = (q & 1) ^ ((hp >> 3) & 1);
-    const int r = hp / p.hw, cc = hp - r * p.hw;
-    const int iy = iy0 + r, ix = ix0 + cc;
-    const int ch = c0 + c * E;
-    const bool ok = hp < hpix && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w && ch < a.ci;
-    const void* src = ok ? (const void*)(xg + ((int64_t)(b * a.h + iy) * a.w + ix) * a.ldx + ch)
-                         : (const void*)g_lic_zero_page;
-    glds16(src, hbuf0 + buf * hbytes + q0 * 16);
-  };
-
   // per-lane halo base pixel of each 32-row m-tile
   int hbase[TM];
 #pragma unroll
@@ -218,18 +179,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
   for (int s = 0; s < nst; ++s) {
     const int k = s / p.ngroups, g = s - k * p.ngroups;
     HSTAMP(st_a);
-#if HALO_INTERLEAVE
-    const int nwp = s + 1 < nst ? w_pieces(s + 1) : 0;
-    const int nhp = (g == 0 && k + 1 < nchunks) ? h_pieces : 0;
-    const int npieces = nwp + nhp;
-    int it_next = 0;
-    auto issue_some = [&](int cnt) {
-      for (int q = 0; q < cnt && it_next < npieces; ++q, ++it_next) {
-        if (it_next < nwp) issue_w_piece(s + 1, (s + 1) & 1, it_next);
-        else issue_h_piece(k + 1, (k + 1) & 1, it_next - nwp);
-      }
-    };
-#elif !(HALO_ABL & 1)
+#if !(HALO_ABL & 1)
 #if !(HALO_ABL & 4)
     if (s + 1 < nst) issue_w(s + 1, (s + 1) & 1);
 #endif
@@ -281,31 +231,17 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
         }
     };
     u32x4 fa[2][TM], fb[2][TN];
-#if HALO_INTERLEAVE
-    // the next stage's pieces go out over the first half of this stage's taps
-    const int span = gcur > 2 ? gcur / 2 : 1;
-    const int per_tap = (npieces + span - 1) / span;
-#define HALO_ISSUE_SOME() issue_some(per_tap)
-#else
-#define HALO_ISSUE_SOME()
-#endif
     load_frags(0, fa[0], fb[0]);
     int tt = 0;
     for (; tt + 2 <= gcur; tt += 2) {
       load_frags(tt + 1, fa[1], fb[1]);
-      HALO_ISSUE_SOME();
       mfmas(fa[0], fb[0]);
       // unconditional (a read past the group's last tap stays inside the LDS
       // allocation and is discarded)
       load_frags(tt + 2, fa[0], fb[0]);
-      HALO_ISSUE_SOME();
       mfmas(fa[1], fb[1]);
     }
     if (tt < gcur) mfmas(fa[0], fb[0]);
-#if HALO_INTERLEAVE
-    issue_some(npieces);
-#endif
-#undef HALO_ISSUE_SOME
     HSTAMP(st_c);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../learning-driven-image-compression-algorithm_amd/csrc"
 make -s
 mkdir -p ../../ab
-OBJS=$(ls build/*.o | grep -v conv_halo_f16)
+OBJS=$(ls build/*.o | grep -v "build/conv_halo_f16.o")
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I."
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
