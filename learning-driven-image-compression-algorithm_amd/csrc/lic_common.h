@@ -374,12 +374,23 @@ __device__ __forceinline__ void epilogue_run(const lic_conv_args& a, const float
       epi_prefetch<T, MASK>(a, rowpix_w + (q / TN) * 32, n0_w + (q % TN) * 32, lane, eo);
     };
     fetch(0, e0);
+    if constexpr (NQ <= 4) {
+      // short: unrolled (a runtime loop here leaves the operand sets in scratch)
+#pragma unroll
+      for (int q = 0; q + 1 < NQ; q += 2) {
+        fetch(q + 1, e1);
+        tile(q, e0);
+        fetch(q + 2, e0);
+        tile(q + 1, e1);
+      }
+    } else {
 #pragma nounroll
-    for (int q = 0; q + 1 < NQ; q += 2) {
-      fetch(q + 1, e1);
-      tile(q, e0);
-      fetch(q + 2, e0);
-      tile(q + 1, e1);
+      for (int q = 0; q + 1 < NQ; q += 2) {
+        fetch(q + 1, e1);
+        tile(q, e0);
+        fetch(q + 2, e0);
+        tile(q + 1, e1);
+      }
     }
     if constexpr (NQ % 2) tile(NQ - 1, e0);
   }
