@@ -3,6 +3,10 @@
 // (instantiated by conv_mfma_*.hip) and conv_halo.h (conv_halo_*.hip).
 #include "lic_common.h"
 
+#ifndef HALO_BIG_TILE
+#define HALO_BIG_TILE 1
+#endif
+
 namespace lic {
 
 // Generic implicit-GEMM launches, instantiated in conv_mfma_*.hip (one TU per
@@ -27,6 +31,12 @@ static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status
   // 16x16 tiles only where at most half of a tile row / column can fall off the map
   const bool big_map = a.mi > 8 && a.mj > 8;
   if (big_map) {
+    // fp16, stride 1: 32x16-pixel tiles halve the weight bytes streamed per FLOP (the
+    // LDS-DMA stream, not the MFMA, bounds the 16x16 tile) where the grid still fills
+    if constexpr (sizeof(T) == 2) {
+      if (HALO_BIG_TILE && a.copad % 192 == 0 && a.isy == 1 && a.isx == 1 && a.mi > 16 && blocks(32, 16, 192) >= 200)
+        return try_halo<T, 32, 16, 192, 4, 2>(a, s, status);
+    }
     if (a.copad % 192 == 0 && blocks(16, 16, 192) >= 200) return try_halo<T, 16, 16, 192, 4, 2>(a, s, status);
     if (a.copad % 128 == 0 && blocks(16, 16, 128) >= 200) return try_halo<T, 16, 16, 128, 4, 2>(a, s, status);
     if (a.copad % 64 == 0 && blocks(16, 16, 64) >= 200) return try_halo<T, 16, 16, 64, 4, 2>(a, s, status);

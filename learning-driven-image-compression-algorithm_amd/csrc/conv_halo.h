@@ -22,6 +22,9 @@
 #ifndef HALO_ABL
 #define HALO_ABL 0
 #endif
+#ifndef HALO_LOADERS
+#define HALO_LOADERS 4
+#endif
 #ifndef HALO_STAMP
 #define HALO_STAMP 0
 #endif
@@ -112,10 +115,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
   const int hq_total = p.hpix_pad * 2;
   const int hpix = p.hh * p.hw;
 
-  auto issue_halo = [&](int k, int buf) {
+  // nw_ld waves move the data, striding by nw_ld * 64 lanes: all waves for the
+  // prologue, HALO_LOADERS waves inside the stage loop (see there)
+  auto issue_halo = [&](int k, int buf, int nw_ld) {
     const int c0 = k * CK;
     char* dst = hbuf0 + buf * hbytes;
-    for (int q0 = wave * 64; q0 < hq_total; q0 += NT) {
+    for (int q0 = wave * 64; q0 < hq_total; q0 += nw_ld * 64) {
       const int q = q0 + lane;
       const int hp = q >> 1;
       const int c = (q & 1) ^ ((hp >> 3) & 1);
@@ -128,14 +133,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
       glds16(src, dst + q0 * 16);
     }
   };
-  auto issue_w = [&](int s, int buf) {
+  auto issue_w = [&](int s, int buf, int nw_ld) {
     const int k = s / p.ngroups, g = s - k * p.ngroups;
     const int c0 = k * CK;
     const int t0 = g * p.G;
     const int gcur = min(p.G, a.ntaps - t0);
     const int total = gcur * BN * 2;
     char* dst = wbuf0 + buf * wbytes;
-    for (int q0 = wave * 64; q0 < total; q0 += NT) {
+    for (int q0 = wave * 64; q0 < total; q0 += nw_ld * 64) {
       const int q = q0 + lane;
       const int tt = q / (BN * 2);
       const int n = (q >> 1) - tt * BN;
@@ -169,8 +174,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
 #endif
   HSTAMP(st_begin);
   if (nst > 0) {
-    issue_halo(0, 0);
-    issue_w(0, 0);
+    issue_halo(0, 0, NT / 64);
+    issue_w(0, 0, NT / 64);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -179,13 +184,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
   for (int s = 0; s < nst; ++s) {
     const int k = s / p.ngroups, g = s - k * p.ngroups;
     HSTAMP(st_a);
+    // Only the first NL waves (one per SIMD when NL = 4: a workgroup's waves are
+    // spread cyclically over the 4 SIMDs) issue the next stage's LDS-DMA; an issuing
+    // wave stalls while the CU's memory pipeline drains its requests, and the
+    // other waves keep the matrix cores busy meanwhile.
+    constexpr int NL = HALO_LOADERS < NT / 64 ? HALO_LOADERS : NT / 64;
 #if !(HALO_ABL & 1)
+    if (wave < NL) {
 #if !(HALO_ABL & 4)
-    if (s + 1 < nst) issue_w(s + 1, (s + 1) & 1);
+      if (s + 1 < nst) issue_w(s + 1, (s + 1) & 1, NL);
 #endif
 #if !(HALO_ABL & 8)
-    if (g == 0 && k + 1 < nchunks) issue_halo(k + 1, (k + 1) & 1);
+      if (g == 0 && k + 1 < nchunks) issue_halo(k + 1, (k + 1) & 1, NL);
 #endif
+    }
 #endif
     HSTAMP(st_b);
     const char* hb = hbuf0 + (k & 1) * hbytes;
