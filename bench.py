@@ -40,6 +40,22 @@ def _env_int(k, d):
         return d
 
 
+PMC_FILE = "profiles/r01/pmc_conv3x3_64.json"
+
+
+def _pmc_traffic(dtype, batch, size):
+    """HBM bytes per launch of the roofline kernel, from the committed PMC passes
+    (rocprofv3 cannot run inside this process); None when the measured
+    configuration differs from this run's."""
+    if dtype != torch.float16 or batch != 32 or size != 256:
+        return None
+    try:
+        with open(os.path.join(ROOT, PMC_FILE)) as f:
+            return int(json.load(f)["traffic_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def build_net(arch, precision, size, batch, device, seed=0):
     from lic_amd.model import net_ga, net_unet_ha_hs
     torch.manual_seed(seed)
@@ -209,9 +225,11 @@ def main():
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"image-sharded x{world} (independent batches, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
-                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} (conv_halo_kernel 16x16 px x 192 ch), "
-                                   f"{flops / 1e9:.1f} GFLOP/launch, {tk * 1e6:.1f} us/launch"},
+                         "frac": round(achieved / peak, 4), "traffic": _pmc_traffic(dtype, args.batch, args.size),
+                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} (conv_halo_kernel, 32x16 px x 192 ch "
+                                   f"tiles), {flops / 1e9:.1f} GFLOP/launch, {tk * 1e6:.1f} us/launch",
+                         "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
+                                         "separate --pmc passes: " + PMC_FILE},
             "a_model": {"ms": round(ta * 1e3, 3), "tflops": round(a_tflops, 2),
                         "frac_of_peak": round(a_tflops / peak, 4),
                         "gflop_per_image": A_MODEL_GFLOP_256 * (args.size / 256) ** 2},
