@@ -56,7 +56,10 @@ enum lic_epilogue {
  * one per output phase (sub-pixel decomposition).  w is packed
  * [copad][ntaps][cpad] in `dtype`, zero-padded (copad >= co, cpad >= ci/groups).
  * out_shuffle=2 writes channel n of pixel (y,x) to channel n/4 of pixel
- * (2y + (n>>1&1), 2x + (n&1)) (conv + nn.PixelShuffle(2)).                    */
+ * (2y + (n>>1&1), 2x + (n&1)) (conv + nn.PixelShuffle(2)).
+ * out_shuffle=3 (phase-major sub-pixel, all four phases of a stride-2 transposed
+ * conv in one launch): with q = co/4, channel n = (2*ry + rx)*q + c of lattice
+ * pixel (y,x) goes to channel c of pixel (2y + ry, 2x + rx).                  */
 typedef struct lic_conv_args {
   int32_t dtype;
   /* input view */
@@ -78,7 +81,7 @@ typedef struct lic_conv_args {
   const void* r1; int32_t ldr1;      /* views with the output's pixel geometry */
   const void* g;  int32_t ldg;
   const void* r2; int32_t ldr2;
-  int32_t out_shuffle;               /* 0 or 2 */
+  int32_t out_shuffle;               /* 0, 2 or 3 */
   int32_t force_direct;              /* testing: force the non-MFMA kernel */
   int32_t force_mfma_generic;        /* testing: skip the spatial-tile (halo) kernel */
 } lic_conv_args;

@@ -186,8 +186,8 @@ extern "C" int lic_conv2d_fwd(const lic_conv_args* a, lic_stream_t stream) {
   if (a->ntaps < 1 || a->ntaps > LIC_MAX_TAPS) return fail("conv: ntaps out of range");
   if (a->groups < 1 || a->ci % a->groups || a->co % a->groups) return fail("conv: bad groups");
   if (a->copad < a->co || a->cpad < a->ci / a->groups) return fail("conv: bad padding of packed weights");
-  if (a->out_shuffle != 0 && a->out_shuffle != 2) return fail("conv: out_shuffle must be 0 or 2");
-  if (a->out_shuffle == 2 && (a->r1 || a->g || a->r2 || a->co % 4)) return fail("conv: shuffle with residual");
+  if (a->out_shuffle != 0 && a->out_shuffle != 2 && a->out_shuffle != 3) return fail("conv: out_shuffle must be 0, 2 or 3");
+  if (a->out_shuffle != 0 && (a->r1 || a->g || a->r2 || a->co % 4)) return fail("conv: shuffle with residual");
   if (a->epi < 0 || a->epi > LIC_EPI_RES_ACT) return fail("conv: bad epilogue");
   if ((a->epi == LIC_EPI_GATE || (a->epi >= LIC_EPI_GDN_DIV && a->epi <= LIC_EPI_GDN_SQRT)) && !a->g) return fail("conv: epilogue needs g");
   if ((a->epi == LIC_EPI_GATE || a->epi == LIC_EPI_HALF_TANH) && !a->r2) return fail("conv: epilogue needs r2");

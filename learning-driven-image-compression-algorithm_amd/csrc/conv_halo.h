@@ -102,7 +102,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
     int base = -1;
     if (i < a.mi && j < a.mj) {
       int oy = a.oy0 + a.osy * i, ox = a.ox0 + a.osx * j;
-      if (a.out_shuffle == 2) { oy *= 2; ox *= 2; }
+      if (a.out_shuffle >= 2) { oy *= 2; ox *= 2; }
       base = (b * a.ho + oy) * a.wo + ox;
     }
     rowpix[m] = base;

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
       int base = -1;
       if (a_ok[r]) {
         int oy = a.oy0 + a.osy * i, ox = a.ox0 + a.osx * j;
-        if (a.out_shuffle == 2) { oy *= 2; ox *= 2; }
+        if (a.out_shuffle >= 2) { oy *= 2; ox *= 2; }
         base = (b * a.ho + oy) * a.wo + ox;
       }
       rowpix[row] = base;

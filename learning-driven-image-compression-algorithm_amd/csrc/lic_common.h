@@ -196,6 +196,11 @@ __device__ __forceinline__ void out_coord(const lic_conv_args& a, int b, int i, 
     oy = 2 * oy + ((n >> 1) & 1);
     ox = 2 * ox + (n & 1);
     ch = n >> 2;
+  } else if (a.out_shuffle == 3) {
+    const int q = a.co >> 2, ph = n / q;
+    oy = 2 * oy + (ph >> 1);
+    ox = 2 * ox + (ph & 1);
+    ch = n - ph * q;
   } else {
     ch = n;
   }
@@ -229,7 +234,8 @@ template <typename T>
 __device__ __forceinline__ bool epi_vec_ok(const lic_conv_args& a) {
   constexpr int V = Vec16<T>::V;
   auto al = [](const void* p, int ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && ld % V == 0); };
-  return a.out_shuffle == 0 && a.co % V == 0 && al(a.y, a.ldy) && al(a.y2, a.ldy2) && al(a.r1, a.ldr1) &&
+  const bool shuf_ok = a.out_shuffle == 0 || (a.out_shuffle == 3 && (a.co >> 2) % V == 0);
+  return shuf_ok && a.co % V == 0 && al(a.y, a.ldy) && al(a.y2, a.ldy2) && al(a.r1, a.ldr1) &&
          al(a.g, a.ldg) && al(a.r2, a.ldr2);
 }
 
@@ -314,8 +320,15 @@ __device__ __forceinline__ void epilogue_tile(const lic_conv_args& a, const floa
     for (int k = 0; k < V; ++k) v[k] = ct[row * 33 + cc * V + k] + bias[k];
     epi_vec<V, (MASK & EPI_R1) != 0>(v, tg, t1, t2, a.epi, a.act, a.slope);
     if (base >= 0 && nok) {
-      store_vec<T>(yg + (int64_t)base * a.ldy + n, v);
-      if (y2g) store_vec<T>(y2g + (int64_t)base * a.ldy2 + n, v);
+      int64_t pix = base;
+      int ch = n;
+      if (a.out_shuffle == 3) {  // phase-major sub-pixel store (vector chunks never straddle phases)
+        const int q = a.co >> 2, ph = n / q;
+        pix += (ph >> 1) * a.wo + (ph & 1);
+        ch = n - ph * q;
+      }
+      store_vec<T>(yg + pix * a.ldy + ch, v);
+      if (y2g) store_vec<T>(y2g + pix * a.ldy2 + ch, v);
     }
   }
 }
@@ -338,6 +351,10 @@ __device__ __forceinline__ void epilogue_tile_scalar(const lic_conv_args& a, con
     if (a.out_shuffle == 2) {
       pix += ((n >> 1) & 1) * a.wo + (n & 1);
       ch = n >> 2;
+    } else if (a.out_shuffle == 3) {
+      const int q = a.co >> 2, ph = n / q;
+      pix += (ph >> 1) * a.wo + (ph & 1);
+      ch = n - ph * q;
     }
     const float v = conv_epilogue<T>(a, ct[erow * 33 + ecol + c], n, pix, ch);
     yg[pix * a.ldy + ch] = from_f<T>(v);

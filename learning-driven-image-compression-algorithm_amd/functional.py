@@ -208,6 +208,40 @@ def pack_conv_transpose2d(weight: torch.Tensor, bias: Optional[torch.Tensor], st
     return packs
 
 
+def pack_conv_transpose2d_fused(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, padding: int,
+                                dtype: torch.dtype, prepad: Tuple[int, int] = (0, 0)) -> Optional[ConvPack]:
+    """All s*s = 4 phases of a stride-2 nn.ConvTranspose2d as ONE conv over the union tap
+    window with 4*co output channels, phase-major (n = (2*ry + rx)*co + c), stored
+    sub-pixel by out_shuffle=3.  Taps a phase does not use carry zero weights.  Returns
+    None when the union window is not a grid of <= LIC_MAX_TAPS taps."""
+    ci, co, kh, kw = weight.shape
+    s, p = stride, padding
+    if s != 2:
+        return None
+    ymaps = [{(r + p - ky) // s - prepad[0]: ky for ky in range(kh) if (r + p - ky) % s == 0} for r in range(s)]
+    xmaps = [{(r + p - kx) // s - prepad[1]: kx for kx in range(kw) if (r + p - kx) % s == 0} for r in range(s)]
+    dys = sorted(set().union(*[m.keys() for m in ymaps]))
+    dxs = sorted(set().union(*[m.keys() for m in xmaps]))
+    if not dys or not dxs or len(dys) * len(dxs) > 64 or dys != list(range(dys[0], dys[-1] + 1)) \
+            or dxs != list(range(dxs[0], dxs[-1] + 1)):
+        return None
+    cpad = _cpad_for(ci, dtype)
+    copad = _choose_copad(4 * co)
+    taps = [(dy, dx) for dy in dys for dx in dxs]
+    w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
+    wt = weight.detach()
+    for ry in range(s):
+        for rx in range(s):
+            ph = 2 * ry + rx
+            for t, (dy, dx) in enumerate(taps):
+                ky, kx = ymaps[ry].get(dy), xmaps[rx].get(dx)
+                if ky is not None and kx is not None:
+                    w[ph * co:(ph + 1) * co, t, :ci] = wt[:, :, ky, kx].t().to(dtype)
+    b = bias.detach().float().repeat(4).contiguous() if bias is not None else None
+    return ConvPack(w=w, bias=b, ci=ci, co=4 * co, dy=[t[0] for t in taps], dx=[t[1] for t in taps],
+                    kh=kh, kw=kw, stride=1)
+
+
 def conv_out_hw(H, W, pk: ConvPack):
     pt, pl, pb, pr = pk.pad
     return (H + pt + pb - pk.kh) // pk.stride + 1, (W + pl + pr - pk.kw) // pk.stride + 1
@@ -241,8 +275,9 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
         Ho, Wo = out.H, out.W
         mi, mj = -(-(Ho - ry) // s), -(-(Wo - rx) // s)
         oy0, ox0, osy, osx, isy, isx = ry, rx, s, s, 1, 1
+    mode = 0 if not shuffle else (2 if shuffle is True else int(shuffle))
     if out is None:
-        if shuffle:
+        if mode:
             out = Act.empty(x.B, Ho * 2, Wo * 2, pk.co // 4, x.dtype, x.t.device)
         else:
             out = Act.empty(x.B, Ho, Wo, pk.co, x.dtype, x.t.device)
@@ -250,7 +285,7 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     a.dtype = dtype_id(x.dtype)
     a.x, a.n, a.h, a.w, a.ci, a.ldx = x.ptr, x.B, x.H, x.W, x.c, x.ld
     a.y, a.ho, a.wo, a.co, a.ldy = out.ptr, out.H, out.W, pk.co, out.ld
-    if shuffle:
+    if mode:
         a.ho, a.wo = out.H, out.W
     a.y2, a.ldy2 = _ptr(y2)
     a.mi, a.mj, a.oy0, a.ox0, a.osy, a.osx, a.isy, a.isx = mi, mj, oy0, ox0, osy, osx, isy, isx
@@ -266,7 +301,7 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     a.r1, a.ldr1 = _ptr(r1)
     a.g, a.ldg = _ptr(g)
     a.r2, a.ldr2 = _ptr(r2)
-    a.out_shuffle = 2 if shuffle else 0
+    a.out_shuffle = mode
     a.force_direct = 1 if force_direct else 0
     a.force_mfma_generic = 1 if force_generic else 0
     check(_lib().lic_conv2d_fwd(ctypes.byref(a), stream_handle()))

@@ -86,13 +86,29 @@ class ConvTranspose2d(nn.ConvTranspose2d, _PackCache):
         return self._get_pack((dtype, prepad), lambda: Fn.pack_conv_transpose2d(
             self.weight, self.bias, self.stride[0], self.padding[0], self.output_padding[0], dtype, prepad))
 
+    def packed_fused(self, dtype: torch.dtype, prepad=(0, 0)):
+        """All four phases in one launch (out_shuffle=3), or None (see pack_conv_transpose2d_fused)."""
+        return self._get_pack((dtype, prepad, "fused"), lambda: Fn.pack_conv_transpose2d_fused(
+            self.weight, self.bias, self.stride[0], self.padding[0], dtype, prepad))
+
     def out_hw(self, H, W, prepad=(0, 0)):
         return Fn.convT_out_hw(H, W, self.stride[0], self.padding[0], self.output_padding[0], self.kernel_size[0],
                                prepad)
 
+    # narrow stride-2 layers (s_model's 192 -> 16 output layer) run as one fused launch:
+    # 4 phases x co channels fill a 64-wide MFMA tile instead of four half-empty ones
+    FUSED_MAX_CO = 16
+
     def run(self, x: Act, out: Optional[Act] = None, *, prepad=(0, 0), **kw) -> Act:
-        packs = self.packed(x.dtype, prepad)
         Ho, Wo = self.out_hw(x.H, x.W, prepad)
+        if (self.stride[0] == 2 and self.out_channels <= self.FUSED_MAX_CO and Ho % 2 == 0 and Wo % 2 == 0
+                and not kw):
+            fpk = self.packed_fused(x.dtype, prepad)
+            if fpk is not None:
+                if out is None:
+                    out = Act.empty(x.B, Ho, Wo, self.out_channels, x.dtype, x.t.device)
+                return Fn.conv(x, fpk, out, out_hw=(Ho // 2, Wo // 2), shuffle=3)
+        packs = self.packed(x.dtype, prepad)
         if self.stride[0] == 1 and self.kernel_size[0] == 1 and self.padding[0] == 0:
             # 1x1 stride-1 transposed conv == 1x1 conv with the transposed weight (one phase).
             return Fn.conv(x, packs[0], out if out is not None else Act.empty(x.B, Ho, Wo, packs[0].co, x.dtype,
