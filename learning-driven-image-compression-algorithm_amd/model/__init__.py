@@ -1,2 +1,2 @@
-from . import net_ga, net_unet_ha_hs
+from . import net_ga, net_unet_ha_hs, source_net
 from .gdn import GDN, IGDN
