@@ -214,7 +214,7 @@ def main():
         ta = time_graph(ga, 10)
         a_tflops = A_MODEL_GFLOP_256 * (args.size / 256) ** 2 * args.batch / ta / 1e3
         result = {
-            "metric": "images/sec encode+decode (256x256)",
+            "metric": f"images/sec encode+decode ({args.size}x{args.size})",
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
