@@ -1,0 +1,145 @@
+"""Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py).
+
+CPU (`not gpu`): the oracle still reproduces every committed vector, and the
+seeded reference-init weights regenerate bit-identically (parameter checksums).
+GPU: the HIP path (through liblic's C ABI) matches the same vectors:
+per-op fp32 at rtol/atol 1e-4, symbols bit-exact given identical (y, mu), and
+end to end bpp within 1e-5 and PSNR within 1e-4 dB (BASELINE.json north_star),
+with the fraction of latent symbols flipped by fp32 summation order < 1e-3.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu as R
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, HERE)
+import make_golden as MG  # noqa: E402
+
+DEV = "cuda"
+
+
+def _load(name):
+    with np.load(os.path.join(HERE, name), allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+# ---------------------------------------------------------------- CPU: oracle pinned to the fixtures
+def test_oracle_reproduces_op_vectors():
+    G = _load("ops.npz")
+    mods = MG.op_modules()
+    x = _t(G["gdn.x"])
+    for name in ("gdn_model", "igdn_model", "gdn_compressai"):
+        P = {"g." + k: v.detach().float() for k, v in mods[name].state_dict().items()}
+        if name == "gdn_compressai":
+            y = R.gdn_compressai(x, P, "g")
+        else:
+            y = R.gdn_model(x, P, "g", inverse=(name == "igdn_model"))
+        torch.testing.assert_close(y, _t(G[name + ".y"]), rtol=1e-6, atol=1e-6)
+    P = {"w." + k: v.detach().float() for k, v in mods["wba"].state_dict().items()}
+    torch.testing.assert_close(R.win_based_attention(_t(G["wba.x"]), P, "w", 8, 4, 2), _t(G["wba.y"]),
+                               rtol=1e-5, atol=1e-6)
+    y, mu, sg = _t(G["rate.y"]), _t(G["rate.mu"]), _t(G["rate.sigma"])
+    assert torch.equal(R.symbols(y, mu), _t(G["rate.symbols"]))
+    assert torch.equal(R.quantize_dequantize(y, mu), _t(G["rate.yhat"]))
+    torch.testing.assert_close(R.gaussian_likelihood(y, sg, mu), _t(G["rate.likelihood"]), rtol=1e-6, atol=1e-12)
+    assert torch.equal(R.ste_round(_t(G["ste.x"])), _t(G["ste.y"]))
+
+
+def test_fixture_ties_are_half_even():
+    """Half of the rate vectors sit exactly on .5 ties; the symbols round them to even."""
+    G = _load("ops.npz")
+    d = G["rate.y"] - G["rate.mu"]
+    ties = np.abs(d - np.floor(d) - 0.5) == 0
+    assert ties.sum() > 100
+    assert np.all(G["rate.symbols"][ties] % 2 == 0)
+    assert list(G["ste.y"][:6]) == [-2.0, -2.0, -0.0, 0.0, 2.0, 2.0]
+
+
+@pytest.mark.parametrize("arch", ["net_ga", "net_unet_ha_hs", "source_net"])
+def test_seeded_weights_regenerate(arch):
+    G = _load(f"{arch}_256.npz")
+    P = MG.state_of(MG.make_net(arch, int(G["size"]), int(G["net_seed"])))
+    s, a = MG.param_sums(P)
+    assert s == G["param_sum"] and a == G["param_abs_sum"], (s, a)
+
+
+def test_oracle_reproduces_source_net_z():
+    G = _load("source_net_256.npz")
+    P = MG.state_of(MG.make_net("source_net"))
+    z = R.source_net_forward(MG.seeded_image(1, int(G["size"]), int(G["x_seed"])), P)
+    torch.testing.assert_close(z, _t(G["z"]), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("arch", ["net_ga", "net_unet_ha_hs"])
+def test_oracle_reproduces_net_vectors(arch):
+    G = _load(f"{arch}_256.npz")
+    P = MG.state_of(MG.make_net(arch))
+    r = R.net_forward(MG.seeded_image(1, int(G["size"]), int(G["x_seed"])), P, arch=arch)
+    assert torch.equal(r["symbols"].to(torch.int16), _t(G["symbols"]))
+    assert abs(r["bpp"].item() - float(G["bpp"])) <= 1e-6
+    assert abs(r["v_psnr"].item() - float(G["v_psnr"])) <= 1e-5
+
+
+# ---------------------------------------------------------------- GPU: HIP path against the fixtures
+@pytest.mark.gpu
+def test_gpu_ops_match_golden():
+    import lic_amd.functional as Fn
+    from lic_amd.functional import Act
+    G = _load("ops.npz")
+    mods = MG.op_modules()
+    x = Act.from_nchw(_t(G["gdn.x"]).to(DEV).contiguous(), torch.float32)
+    for name in ("gdn_model", "igdn_model", "gdn_compressai"):
+        y = mods[name].to(DEV).run(x).nchw().cpu()
+        torch.testing.assert_close(y, _t(G[name + ".y"]), rtol=1e-4, atol=1e-4)
+    xw = Act.from_nchw(_t(G["wba.x"]).to(DEV).contiguous(), torch.float32)
+    y = mods["wba"].to(DEV).run(xw).nchw().cpu()
+    torch.testing.assert_close(y, _t(G["wba.y"]), rtol=1e-4, atol=1e-4)
+    # rate kernel on NHWC views of the same values
+    nhwc = lambda k: Act(_t(G[k]).permute(0, 2, 3, 1).contiguous().to(DEV))
+    Y, MU, SC = nhwc("rate.y"), nhwc("rate.mu"), nhwc("rate.sigma")
+    B, H, W, C = Y.t.shape
+    sym = torch.empty(B, H, W, C, dtype=torch.int32, device=DEV)
+    lik = torch.empty(B, H, W, C, dtype=torch.float32, device=DEV)
+    yq = Act.empty(B, H, W, C, torch.float32, DEV)
+    parts = torch.zeros(1024, dtype=torch.float64, device=DEV)
+    Fn.gauss_rate(Y, MU, SC, parts, 0, yq=yq, symbols=Act(sym), likelihood=Act(lik))
+    to_nchw = lambda t: t.permute(0, 3, 1, 2).cpu()
+    assert torch.equal(to_nchw(sym), _t(G["rate.symbols"]))
+    assert torch.equal(to_nchw(yq.t), _t(G["rate.yhat"]))
+    torch.testing.assert_close(to_nchw(lik), _t(G["rate.likelihood"]), rtol=2e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch", ["net_ga", "net_unet_ha_hs"])
+def test_gpu_net_matches_golden(arch):
+    G = _load(f"{arch}_256.npz")
+    net = MG.make_net(arch).to(DEV)
+    x = MG.seeded_image(1, int(G["size"]), int(G["x_seed"])).to(DEV)
+    bpp, v_mse, v_psnr = net(x, "test", return_intermediates=True)
+    sym = net.last["symbols"].cpu().to(torch.int16)
+    mism = (sym != _t(G["symbols"])).float().mean().item()
+    print(f"\n[{arch} golden] bpp {bpp.item():.8f} / {float(G['bpp']):.8f} psnr {v_psnr.item():.6f} / "
+          f"{float(G['v_psnr']):.6f} symbols flipped {mism:.2e}")
+    assert mism < 1e-3
+    assert abs(bpp.item() - float(G["bpp"])) <= 1e-5 * max(1.0, abs(float(G["bpp"])))
+    assert abs(v_psnr.item() - float(G["v_psnr"])) <= 1e-4 or math.isinf(float(G["v_psnr"]))
+
+
+@pytest.mark.gpu
+def test_gpu_source_net_matches_golden():
+    G = _load("source_net_256.npz")
+    net = MG.make_net("source_net").to(DEV)
+    z = net(MG.seeded_image(1, int(G["size"]), int(G["x_seed"])).to(DEV), "test").float().cpu()
+    ref = _t(G["z"])
+    rel = ((z - ref).abs().max() / ref.abs().max()).item()
+    assert rel < 1e-4, rel
