@@ -109,7 +109,8 @@ def make_ops():
     out["rate.y"], out["rate.mu"], out["rate.sigma"] = y, mu, sigma
     out["rate.symbols"] = R.symbols(y, mu)
     out["rate.yhat"] = R.quantize_dequantize(y, mu)
-    out["rate.likelihood"] = R.gaussian_likelihood(y, sigma, mu)
+    # compressai GaussianConditional.forward prices the quantized outputs (net_ga.py:1049)
+    out["rate.likelihood"] = R.gaussian_likelihood(out["rate.yhat"], sigma, mu)
     t = torch.tensor([-2.5, -1.5, -0.5, 0.5, 1.5, 2.5, 0.49999997, -0.49999997])
     out["ste.x"], out["ste.y"] = t, R.ste_round(t)
     np.savez(os.path.join(HERE, "ops.npz"), **{k: v.numpy() for k, v in out.items()})

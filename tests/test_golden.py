@@ -51,7 +51,7 @@ def test_oracle_reproduces_op_vectors():
     y, mu, sg = _t(G["rate.y"]), _t(G["rate.mu"]), _t(G["rate.sigma"])
     assert torch.equal(R.symbols(y, mu), _t(G["rate.symbols"]))
     assert torch.equal(R.quantize_dequantize(y, mu), _t(G["rate.yhat"]))
-    torch.testing.assert_close(R.gaussian_likelihood(y, sg, mu), _t(G["rate.likelihood"]), rtol=1e-6, atol=1e-12)
+    torch.testing.assert_close(R.gaussian_likelihood(R.quantize_dequantize(y, mu), sg, mu), _t(G["rate.likelihood"]), rtol=1e-6, atol=1e-12)
     assert torch.equal(R.ste_round(_t(G["ste.x"])), _t(G["ste.y"]))
 
 
