@@ -8,9 +8,21 @@ unsynchronised, :93-100); no PNG side effects; ``--all-images`` evaluates every 
 select the model file and the activation dtype; a missing checkpoint falls back to the
 reference's seeded initialisation with a warning (no checkpoints ship with the reference).
 ``--pre_processing`` (online finetune) needs the training path and is not available yet.
+
+BASELINE config 4 (Kodak-24 R-D sweep, image-sharded over 1/2/4/8 GPUs):
+``--synthetic-kodak`` stands in for the Kodak PNGs (none ship with the reference and
+there is no network): 24 seeded smooth images with Kodak's shapes (18 landscape
+768x512, 6 portrait 512x768 at Kodak's portrait indices).  ``--lambdas`` sweeps the
+reference's lambda list; with no checkpoints each lambda's weights are the seeded
+reference initialisation with seed = lambda index, or
+``--weight_path`` may contain ``{lmbda}``.  ``--graph`` replays one captured hipGraph
+per (lambda, image shape).  Rank 0 prints one JSON summary line (images/s of the sweep,
+whole job, elapsed = MAX over ranks).
 """
 import argparse
 import glob
+import json
+import math
 import os
 import sys
 import time
@@ -36,6 +48,101 @@ def pad64(data):
     data = torch.cat((data, torch.ones(3, hp - h, w)), 1)
     data = torch.cat((data, torch.ones(3, hp, wp - w)), 2)
     return data, h, w
+
+
+KODAK_PORTRAIT = (3, 8, 9, 16, 17, 18)   # 0-based indices of Kodak's 512x768 (portrait) images
+RD_LAMBDAS = (0.0018, 0.0035, 0.0067, 0.0130, 0.0250, 0.0483, 0.0932)
+
+
+def synthetic_image(idx, h, w):
+    """Seeded smooth stand-in for a natural image: a sum of random low-frequency
+    sinusoids per channel plus mild noise, in [0, 1]."""
+    g = torch.Generator().manual_seed(1000 + idx)
+    yy = torch.linspace(0, 1, h).view(h, 1)
+    xx = torch.linspace(0, 1, w).view(1, w)
+    img = torch.zeros(3, h, w)
+    for c in range(3):
+        for _ in range(6):
+            fy, fx = (torch.rand(2, generator=g) * 8).tolist()
+            ph, amp = (torch.rand(2, generator=g) * torch.tensor([2 * math.pi, 0.25])).tolist()
+            img[c] += amp * torch.sin(2 * math.pi * (fy * yy + fx * xx) + ph)
+    img = 0.5 + img + 0.03 * torch.randn(3, h, w, generator=g)
+    return img.clamp(0, 1)
+
+
+def synthetic_kodak():
+    """24 (name, [3,H,W] in [0,1]) pairs with Kodak-24's shapes."""
+    return [(f"synthetic_kodim{i + 1:02d}", synthetic_image(i, *((768, 512) if i in KODAK_PORTRAIT else (512, 768))))
+            for i in range(24)]
+
+
+def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=False, graph=True, reps=1,
+             device="cuda"):
+    """BASELINE config 4: every lambda x every synthetic Kodak image, images sharded
+    round-robin over ranks.  Returns (per-lambda summaries, images/s) on rank 0."""
+    from lic_amd.model import net_ga, net_unet_ha_hs
+    from lic_amd import distributed as D
+    mod = net_ga if arch == "net_ga" else net_unet_ha_hs
+    rank, world, local = D.init("nccl")
+    if world > 1 or torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    mine = D.shard(synthetic_kodak(), rank, world)
+    summaries, total_time = [], 0.0
+    for li, lmbda in enumerate(lambdas):
+        nets, graphs = {}, {}
+        sums = [0.0, 0.0, 0.0, 0.0]  # bpp, psnr, mse, rd
+        for name, img in mine:
+            _, h, w = img.shape
+            data, h, w = pad64(img)
+            x = (data.unsqueeze(0) * 2.0 - 1.0).to(device)
+            key = tuple(x.shape)
+            if key not in nets:
+                torch.manual_seed(li)
+                net = mod.Net((1, h, w, 3), (1, h, w, 3), is_high, False, precision=precision).to(device)
+                wp = weight_path.format(lmbda=lmbda) if weight_path else ""
+                if wp and os.path.exists(wp):
+                    net.load_state_dict(torch.load(wp, map_location="cpu", weights_only=True), strict=True)
+                xin = torch.empty_like(x)
+                nets[key] = (net, xin)
+                if graph:
+                    xin.copy_(x)
+                    net(xin, 'test')
+                    s = torch.cuda.Stream()
+                    s.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(s):
+                        net(xin, 'test')
+                    torch.cuda.current_stream().wait_stream(s)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        out = net(xin, 'test')
+                    graphs[key] = (g, out)
+            net, xin = nets[key]
+            xin.copy_(x)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                if graph:
+                    graphs[key][0].replay()
+                    bpp, v_mse, v_psnr = graphs[key][1]
+                else:
+                    bpp, v_mse, v_psnr = net(xin, 'test')
+            torch.cuda.synchronize()
+            total_time += (time.perf_counter() - t0) / reps
+            b, m, p = bpp.item(), v_mse.mean().item(), v_psnr.item()
+            sums[0] += b; sums[1] += p; sums[2] += m; sums[3] += b + lmbda * m
+        sums = D.sum_over_ranks(sums + [len(mine)], world, device)
+        cnt = sums[4]
+        summaries.append({"lambda": lmbda, "bpp": sums[0] / cnt, "psnr": sums[1] / cnt, "mse": sums[2] / cnt,
+                          "rd": sums[3] / cnt, "images": int(cnt)})
+        if rank == 0:
+            print('[lambda %.4f] bpp: %.4f psnr: %.4f v_mse: %.4f bpp+lambda*mse: %.4f' % (
+                lmbda, sums[0] / cnt, sums[1] / cnt, sums[2] / cnt, sums[3] / cnt), flush=True)
+    # elapsed = slowest rank's forward time; images = all ranks' images over the sweep
+    elapsed = D.max_over_ranks(total_time, world, device)
+    n_img = len(lambdas) * 24
+    D.finish(world)
+    return summaries, n_img / elapsed, world
 
 
 def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing, tune_iter, arch="net_ga",
@@ -103,7 +210,23 @@ def main(argv=None):
     parser.add_argument("--arch", default="net_ga", choices=["net_ga", "net_unet_ha_hs"])
     parser.add_argument("--precision", default="fp32", choices=["fp32", "fp16"])
     parser.add_argument("--all-images", action="store_true", dest="all_images")
+    parser.add_argument("--synthetic-kodak", action="store_true", dest="synthetic_kodak",
+                        help="BASELINE config 4: R-D sweep over 24 synthetic Kodak-shaped images")
+    parser.add_argument("--lambdas", default=",".join(str(v) for v in RD_LAMBDAS),
+                        help="comma-separated lambda list for --synthetic-kodak")
+    parser.add_argument("--graph", action="store_true", help="hipGraph replay per (lambda, shape)")
     args = parser.parse_args(argv)
+    if args.synthetic_kodak:
+        lambdas = [float(v) for v in args.lambdas.split(",") if v]
+        summ, ips, world = rd_sweep(lambdas, args.weight_path, arch=args.arch, precision=args.precision,
+                                    is_high=args.high, graph=args.graph)
+        if int(os.environ.get("RANK", 0)) == 0:
+            print(json.dumps({"metric": "images/sec encode+decode (Kodak-24 R-D sweep, 768x512)",
+                              "value": round(ips, 2), "unit": "images/s", "n_gpus": world,
+                              "arch": args.arch, "precision": args.precision, "graph": args.graph,
+                              "data": "synthetic Kodak-shaped images, seeded weights per lambda",
+                              "rd": summ}), flush=True)
+        return
     print(args.weight_path)
     val(args.data_path, args.weight_path, args.lmbda, args.high, args.post_processing, args.pre_processing,
         args.tune_iter, arch=args.arch, precision=args.precision, all_images=args.all_images)
