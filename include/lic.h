@@ -198,6 +198,81 @@ int lic_copy(int32_t dtype_in, const void* x, int32_t ldx, int32_t npix, int32_t
 int lic_avgpool(int32_t dtype, const void* x, int32_t n, int32_t hw, int32_t c, int32_t ldx,
                 void* y, int32_t ldy, lic_stream_t stream);
 
+/* ---- Entropy coder ---------------------------------
+ * The reference only ESTIMATES the rate (net_ga.py:1049 likelihoods, :1104-1107
+ * bpp) and never writes a bitstream.  These entry points are the coder of its
+ * entropy models' library (compressai 1.2.x, unvendored): CDF tables built as
+ * GaussianConditional.update / EntropyBottleneck.update do, and the Rans64 coder of
+ * BufferedRansEncoder::encode_with_indexes / RansDecoder::decode_with_indexes
+ * (precision 16, 4-bit bypass chunks for values outside a table).  A latent is
+ * coded as independent streams, one per (image, channel), symbols in raster
+ * order; each stream is exactly the compressai string of that symbol list.
+ * CDF tables are [ntab][cdf_stride] int32 with cdf_sizes[t] = pmf length + 2
+ * and offsets[t] = the symbol value of table entry 0.                          */
+
+/* Gaussian pmfs of compressai GaussianConditional.update(): table t has
+ * 2*pmf_center[t]+1 entries pmf[k] = Phi((.5-|k-c|)/s) - Phi((-.5-|k-c|)/s)
+ * followed by the tail mass 2*Phi((-.5-c)/s); rows of pmf_stride floats. */
+int lic_gauss_pmf(const float* scale_table, const int32_t* pmf_center, int32_t ntab, int32_t pmf_stride,
+                  float* pmf, lic_stream_t stream);
+
+/* Factorized-prior pmfs of compressai EntropyBottleneck.update() for the
+ * default filters (3,3,3,3): params is [c][LIC_EB_PARAMS] fp32 per channel
+ * (matrix0..4, bias0..4, factor0..3 flattened in that order, raw parameters:
+ * softplus / tanh are applied here); pmf_start[c] = median - minima,
+ * pmf_length[c] entries then the tail mass.  pmf_stride must be
+ * max(pmf_length) + 1: the upper tail is evaluated at sample pmf_stride - 2 for
+ * every channel, as compressai does on its padded sample grid. */
+#define LIC_EB_PARAMS 58
+int lic_eb_pmf(const float* params, const float* pmf_start, const int32_t* pmf_length, int32_t c,
+               int32_t pmf_stride, float* pmf, lic_stream_t stream);
+
+/* compressai pmf_to_quantized_cdf per table: nsym[t] pmf entries (tail included)
+ * -> nsym[t]+1 cdf entries at `precision` bits.  status[t] = 0, or 1 when no
+ * frequency could be stolen (degenerate pmf). */
+int lic_pmf_to_cdf(const float* pmf, const int32_t* nsym, int32_t ntab, int32_t pmf_stride, int32_t precision,
+                   int32_t* cdf, int32_t cdf_stride, int32_t* status, lic_stream_t stream);
+
+/* GaussianConditional.build_indexes: idx = ntab-1 - #{t < ntab-1 : max(scale, bound) <= table[t]}. */
+int lic_gauss_indexes(int32_t dtype, const void* scales, int32_t npix, int32_t c, int32_t ldsc,
+                      const float* scale_table, int32_t ntab, float bound, int32_t* idx, int32_t ldidx,
+                      lic_stream_t stream);
+
+/* symbols = (int) round_half_even(z - m[c]) (EntropyModel.quantize(..., "symbols", medians));
+ * medians may be NULL (0). */
+int lic_quantize_symbols(int32_t dtype, const void* z, int32_t npix, int32_t c, int32_t ldz, const float* medians,
+                         int32_t* sym, int32_t ldsym, lic_stream_t stream);
+
+/* Streams: s = b * ctot + c0 + ch for image b < n, channel ch < c; hw symbols each
+ * at pixel rows [b*hw, (b+1)*hw) of the channel-window views. */
+typedef struct lic_rans_args {
+  int32_t n, hw, c, ctot, c0;
+  const int32_t* symbols; int32_t ldsym;      /* encode: input */
+  const int32_t* indexes; int32_t ldidx;      /* NULL: table index = channel (c0 + ch) */
+  const int32_t* cdfs; int32_t cdf_stride;
+  const int32_t* cdf_sizes; const int32_t* offsets; int32_t ncdf;
+  /* encode: per-stream scratch [n*ctot][cap] words; the string ends at the row end */
+  uint32_t* scratch; int32_t cap; int32_t* lengths;   /* words, -1 = overflow / bad index */
+  /* decode: stream s occupies words[offsets_w[s] .. offsets_w[s+1]) */
+  const uint32_t* words; const uint32_t* offsets_w;
+  int32_t dtype;                              /* of mu / yq */
+  int32_t* out_symbols; int32_t ldosym;       /* decode outputs (each may be NULL) */
+  const void* mu; int32_t ldmu;               /* per-element means (dtype) or NULL */
+  const float* mu_ch;                         /* per-channel means (medians) or NULL */
+  void* yq; int32_t ldyq;                     /* (float)symbol + mean, as lic_gauss_rate_fwd */
+  int32_t* status;                            /* decode: [n*c] 0 ok, 1 = the stream ended early or
+                                                 named an invalid table (rANS cannot detect other
+                                                 corruption; reads never pass the stream's end) */
+} lic_rans_args;
+/* Upper bound of the words a stream of hw symbols can take (scratch row size). */
+int32_t lic_rans_cap(int32_t hw);
+int lic_rans_encode(const lic_rans_args* a, lic_stream_t stream);
+/* Exclusive scan of lengths[nstreams] into offsets_w[nstreams+1] and copy of every
+ * scratch string to out (capacity nstreams*cap words).  Lengths must be >= 0. */
+int lic_rans_pack(const uint32_t* scratch, int32_t cap, const int32_t* lengths, int32_t nstreams,
+                  uint32_t* offsets_w, uint32_t* out, lic_stream_t stream);
+int lic_rans_decode(const lic_rans_args* a, lic_stream_t stream);
+
 /* Library info. */
 const char* lic_last_error(void);
 const char* lic_version(void);

@@ -24,7 +24,10 @@ EXPORTED_SYMBOLS = (
     "lic_gauss_rate_fwd", "lic_quantize_median", "lic_bpp_finalize", "lic_syntax_recon_fwd",
     "lic_psnr_finalize", "lic_nchw_to_nhwc", "lic_nhwc_to_nchw", "lic_add", "lic_copy",
     "lic_avgpool", "lic_rb3_fwd", "lic_last_error", "lic_version", "lic_device_arch",
+    "lic_gauss_pmf", "lic_eb_pmf", "lic_pmf_to_cdf", "lic_gauss_indexes", "lic_quantize_symbols",
+    "lic_rans_cap", "lic_rans_encode", "lic_rans_pack", "lic_rans_decode",
 )
+LIC_EB_PARAMS = 58
 
 
 class LicError(RuntimeError):
@@ -86,6 +89,24 @@ class RateArgs(ctypes.Structure):
     ]
 
 
+class RansArgs(ctypes.Structure):
+    _fields_ = [
+        ("n", _i32), ("hw", _i32), ("c", _i32), ("ctot", _i32), ("c0", _i32),
+        ("symbols", _vp), ("ldsym", _i32),
+        ("indexes", _vp), ("ldidx", _i32),
+        ("cdfs", _vp), ("cdf_stride", _i32),
+        ("cdf_sizes", _vp), ("offsets", _vp), ("ncdf", _i32),
+        ("scratch", _vp), ("cap", _i32), ("lengths", _vp),
+        ("words", _vp), ("offsets_w", _vp),
+        ("dtype", _i32),
+        ("out_symbols", _vp), ("ldosym", _i32),
+        ("mu", _vp), ("ldmu", _i32),
+        ("mu_ch", _vp),
+        ("yq", _vp), ("ldyq", _i32),
+        ("status", _vp),
+    ]
+
+
 _lib = None
 _load_error = None
 
@@ -123,11 +144,21 @@ def load():
         "lic_copy": [I, V, I, I, I, I, V, I, V],
         "lic_avgpool": [I, V, I, I, I, I, V, I, V],
         "lic_device_arch": [V, I],
+        "lic_gauss_pmf": [V, V, I, I, V, V],
+        "lic_eb_pmf": [V, V, V, I, I, V, V],
+        "lic_pmf_to_cdf": [V, V, I, I, I, V, I, V, V],
+        "lic_gauss_indexes": [I, V, I, I, I, V, I, F, V, I, V],
+        "lic_quantize_symbols": [I, V, I, I, I, V, V, I, V],
+        "lic_rans_encode": [V, V],
+        "lic_rans_pack": [V, I, V, I, V, V, V],
+        "lic_rans_decode": [V, V],
     }
     for name, argt in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = argt
         fn.restype = ctypes.c_int
+    lib.lic_rans_cap.argtypes = [I]
+    lib.lic_rans_cap.restype = ctypes.c_int32
     lib.lic_last_error.restype = ctypes.c_char_p
     lib.lic_version.restype = ctypes.c_char_p
     _lib = lib

@@ -413,14 +413,18 @@ class Net(nn.Module):
         (the two hyper-synthesis stacks run concurrently)."""
         z = _run_seq_gelu(self.h_a, z3)
         z_hat = Fn.quantize_median(z, self._medians(z.t.device))
-        main = torch.cuda.current_stream(z.t.device)
-        side = self._side_stream(z.t.device, 1)
+        self._hyper_s(z_hat, means_out, scales_out)
+        return z, z_hat
+
+    def _hyper_s(self, z_hat: Act, means_out: Act, scales_out: Act):
+        """latent_means / latent_scales from z_hat (the decoder side of :1004-1007)."""
+        main = torch.cuda.current_stream(z_hat.t.device)
+        side = self._side_stream(z_hat.t.device, 1)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             _run_seq_gelu(self.h_scale_s, z_hat, scales_out)
         _run_seq_gelu(self.h_mean_s, z_hat, means_out)
         main.wait_stream(side)
-        return z, z_hat
 
     def _medians(self, device):
         """EntropyBottleneck._get_medians() flattened to [C] fp32 (cached per parameter version)."""
@@ -473,6 +477,162 @@ class Net(nn.Module):
     def dtype(self):
         return torch.float16 if self.precision == "fp16" else torch.float32
 
+    def _slice_buffers(self, B, hh, ww, dt, dev):
+        sw = 192 // self.num_slices
+        LR = Act.empty(B, hh, ww, 192 + sw * 4, dt, dev)           # lrp_support (widest: 384)
+        MU = Act.empty(B, hh, ww, 192, dt, dev)
+        SC = Act.empty(B, hh, ww, 192, dt, dev)
+        SYM = torch.empty((B, hh, ww, 192), dtype=torch.int32, device=dev)
+        nper = -(-(B * hh * ww * sw) // 256)
+        partials = torch.empty((self.num_slices * nper,), dtype=torch.float64, device=dev)
+        return LR, MU, SC, SYM, partials, nper
+
+    def _slice_loop(self, z3: Optional[Act], MS: Act, SS: Act, LR: Act, MU: Act, SC: Act, SYM: torch.Tensor,
+                    LIK: Optional[torch.Tensor], partials: torch.Tensor, nper: int, decode=None):
+        """net_ga.py:1028-1062.  Encoder / forward: y_i is quantised against mu_i and priced
+        (lic_gauss_rate_fwd).  Decoder (``decode(i, mu, scale, yq_out, sym_out)``): the
+        slice's symbols come from the bitstream instead of z3."""
+        dev = MS.t.device
+        ns, sw = self.num_slices, 192 // self.num_slices
+        main = torch.cuda.current_stream(dev)
+        side2 = self._side_stream(dev, 1)
+        for i in range(ns):
+            ci = 192 + sw * min(i, 4)
+            # the scale branch (:1042-1046) is independent of the mean branch (:1034-1040)
+            side2.wait_stream(main)
+            with torch.cuda.stream(side2):
+                ss = self.atten_scale[i][0].run(SS.ch(0, ci))
+                cs = self.cc_scale_transforms[i]
+                t = cs[0].run(ss, act=ACT_GELU)
+                t = cs[2].run(t, act=ACT_GELU)
+                sc = cs[4].run(t, out=SC.ch(sw * i, sw * (i + 1)))
+            ms = self.atten_mean[i][0].run(MS.ch(0, ci), out=LR.ch(0, ci))
+            cm = self.cc_mean_transforms[i]
+            t = cm[0].run(ms, act=ACT_GELU)
+            t = cm[2].run(t, act=ACT_GELU)
+            mu = cm[4].run(t, out=MU.ch(sw * i, sw * (i + 1)))
+            main.wait_stream(side2)
+            yq = LR.ch(ci, ci + sw)
+            if decode is None:
+                Fn.gauss_rate(z3.ch(sw * i, sw * (i + 1)), mu, sc, partials, i * nper, yq=yq,
+                              symbols=Act(SYM, sw * i, sw),
+                              likelihood=Act(LIK, sw * i, sw) if LIK is not None else None,
+                              scale_bound=self.gaussian_conditional._scale_bound,
+                              likelihood_bound=self.gaussian_conditional._likelihood_bound)
+            else:
+                decode(i, mu, sc, yq, Act(SYM, sw * i, sw))
+            lr = self.lrp_transforms[i]
+            t = lr[0].run(LR.ch(0, ci + sw), act=ACT_GELU)
+            t = lr[2].run(t, act=ACT_GELU)
+            y2 = SS.ch(192 + sw * i, 192 + sw * (i + 1)) if (not self._shared_support and i < ns - 1) else None
+            lr[4].run(t, out=MS.ch(192 + sw * i, 192 + sw * (i + 1)), epi=EPI_HALF_TANH, r2=yq, y2=y2)
+
+    # ---- entropy coding (SURVEY.md 8(f) rank 2; compressai CompressionModel API)
+    _codable = True
+
+    def update(self, scale_table=None, force: bool = False) -> bool:
+        """CompressionModel.update: build the Gaussian (scale table, default 64 levels
+        0.11..256) and factorized-prior (EntropyBottleneck) CDF tables on the device."""
+        from .. import entropy_coder as EC
+        dev = self.entropy_bottleneck.quantiles.device
+        eb = self.entropy_bottleneck
+        key = (str(dev), eb.quantiles._version, eb.quantiles.data_ptr(),
+               tuple(getattr(eb, n)._version for n in EC._EB_ORDER))
+        cur = self.__dict__.get("_coder")
+        if cur is not None and cur[0] == key and not force and scale_table is None:
+            return False
+        st = (EC.get_scale_table() if scale_table is None else torch.as_tensor(scale_table).float()).to(dev)
+        gt = EC.gauss_tables(st)
+        et, med = EC.eb_tables(eb)
+        gt.check()
+        et.check()
+        self.__dict__["_coder"] = (key, dict(scale_table=st.contiguous(), gauss=gt, eb=et, medians=med))
+        return True
+
+    def _coder_state(self):
+        if not self._codable:
+            raise NotImplementedError(
+                f"{self.arch}: h_s consumes encoder-side features (net_unet_ha_hs.py:880-895), so its "
+                "latents cannot be decoded from a bitstream; use net_ga")
+        self.update()
+        return self.__dict__["_coder"][1]
+
+    @torch.no_grad()
+    def compress(self, inputs: torch.Tensor):
+        """Encode a batch to bitstreams: {"strings": [y_strings, z_strings], "shape": z's (h, w),
+        "syntax": int32 [B, M]} (one bytes string per image in each list)."""
+        from .. import entropy_coder as EC
+        if not inputs.is_cuda:
+            raise RuntimeError("lic_amd Net runs on the GPU only (HIP path); move inputs to cuda")
+        cs = self._coder_state()
+        x_in = inputs.contiguous().float()
+        B = x_in.shape[0]
+        dev, dt = x_in.device, self.dtype
+        z3 = self.a_model.run(Act.from_nchw(x_in, dt, pad16=True))
+        hh, ww = z3.H, z3.W
+        syn_r = self.syntax_model.run(z3.ch(0, self.M))
+        MS = Act.empty(B, hh, ww, 192 + 192, dt, dev)
+        SS = MS if self._shared_support else Act.empty(B, hh, ww, 192 + 144, dt, dev)
+        z, z_hat = self._hyper(z3, MS.ch(0, 192), SS.ch(0, 192))
+        LR, MU, SC, SYM, partials, nper = self._slice_buffers(B, hh, ww, dt, dev)
+        self._slice_loop(z3, MS, SS, LR, MU, SC, SYM, None, partials, nper)
+        ZS = torch.empty((B, z.H, z.W, z.c), dtype=torch.int32, device=dev)
+        EC.quantize_symbols(z, cs["medians"], Act(ZS))
+        zwords, zoff = EC.encode_streams(Act(ZS), None, cs["eb"])
+        IDX = torch.empty((B, hh, ww, 192), dtype=torch.int32, device=dev)
+        EC.gauss_indexes(SC, cs["scale_table"], self.gaussian_conditional._scale_bound, Act(IDX))
+        ywords, yoff = EC.encode_streams(Act(SYM), Act(IDX), cs["gauss"])
+        # the rounded syntax vector (net_ga.py:1016) travels as M int32 side values per image
+        syntax = syn_r.nchw().reshape(B, self.M).float().to(torch.int32)
+        return {"strings": [EC.to_strings(ywords, yoff, B, 192), EC.to_strings(zwords, zoff, B, z.c)],
+                "shape": (z.H, z.W), "syntax": syntax.cpu(), "symbols": SYM}
+
+    @torch.no_grad()
+    def decompress(self, strings, shape, syntax: torch.Tensor, device="cuda"):
+        """Decode bitstreams from compress() -> {"x_hat": [B, 3, H, W] fp32 in [-1, 1],
+        "symbols": int32 [B, h, w, 192]}; raises on a corrupt stream."""
+        from .. import entropy_coder as EC
+        y_strings, z_strings = strings
+        cs = self._coder_state()
+        dev = torch.device(device)
+        dt = self.dtype
+        B = len(y_strings)
+        zh, zw = shape
+        zc = self._eb_channels
+        status = torch.zeros((B * 192,), dtype=torch.int32, device=dev)
+        zwords, zoff = EC.from_strings(z_strings, zc, dev)
+        z_hat = Act.empty(B, zh, zw, zc, dt, dev)
+        EC.decode_streams(zwords, zoff, cs["eb"], B, zh * zw, zc, 0, zc, yq=z_hat, mu_ch=cs["medians"],
+                          status=status)
+        hh, ww = zh * 4, zw * 4
+        MS = Act.empty(B, hh, ww, 192 + 192, dt, dev)
+        SS = MS if self._shared_support else Act.empty(B, hh, ww, 192 + 144, dt, dev)
+        self._hyper_s(z_hat, MS.ch(0, 192), SS.ch(0, 192))
+        ywords, yoff = EC.from_strings(y_strings, 192, dev)
+        LR, MU, SC, SYM, partials, nper = self._slice_buffers(B, hh, ww, dt, dev)
+        sw = 192 // self.num_slices
+        IDX = torch.empty((B, hh, ww, sw), dtype=torch.int32, device=dev)
+        ystat = torch.zeros((self.num_slices, B * sw), dtype=torch.int32, device=dev)
+
+        def dec(i, mu, sc, yq, sym):
+            EC.gauss_indexes(sc, cs["scale_table"], self.gaussian_conditional._scale_bound, Act(IDX))
+            EC.decode_streams(ywords, yoff, cs["gauss"], B, hh * ww, 192, sw * i, sw, idx=Act(IDX), yq=yq,
+                              mu=mu, symbols=sym, status=ystat[i])
+
+        self._slice_loop(None, MS, SS, LR, MU, SC, SYM, None, partials, nper, decode=dec)
+        if int(status[:B * zc].sum()) or int(ystat.sum()):
+            raise ValueError("decompress: corrupt bitstream")
+        x_tilde = self.s_model.run(MS.ch(192, 384))
+        syn = Act(syntax.to(dev).to(dt).reshape(B, 1, 1, self.M).contiguous())
+        cw = self.conv_weights_gen.run(syn)
+        H, W = hh * 16, ww * 16
+        x_rec = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
+        ppi = max(1, min(64, -(-(H * W) // 4096)))
+        sq_parts = torch.empty((B * ppi,), dtype=torch.float64, device=dev)
+        zeros = torch.zeros((B, 3, H, W), dtype=torch.float32, device=dev)
+        Fn.syntax_recon(x_tilde, cw, zeros, x_rec, sq_parts, ppi)
+        return {"x_hat": x_rec, "symbols": SYM}
+
     # ---- forward
     @torch.no_grad()
     def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False):
@@ -503,41 +663,9 @@ class Net(nn.Module):
         MS = Act.empty(B, hh, ww, 192 + 192, dt, dev)
         SS = MS if self._shared_support else Act.empty(B, hh, ww, 192 + 144, dt, dev)
         z, z_hat = self._hyper(z3, MS.ch(0, 192), SS.ch(0, 192))
-        side2 = self._side_stream(dev, 1)
-        LR = Act.empty(B, hh, ww, 192 + sw * 4, dt, dev)           # lrp_support (widest: 384)
-        MU = Act.empty(B, hh, ww, 192, dt, dev)
-        SC = Act.empty(B, hh, ww, 192, dt, dev)
-        SYM = torch.empty((B, hh, ww, 192), dtype=torch.int32, device=dev)
+        LR, MU, SC, SYM, partials, nper = self._slice_buffers(B, hh, ww, dt, dev)
         LIK = torch.empty((B, hh, ww, 192), dtype=torch.float32, device=dev) if return_intermediates else None
-        nper = -(-(B * hh * ww * sw) // 256)
-        partials = torch.empty((ns * nper,), dtype=torch.float64, device=dev)
-        for i in range(ns):                                        # net_ga.py:1028-1062
-            ci = 192 + sw * min(i, 4)
-            # the scale branch (:1042-1046) is independent of the mean branch (:1034-1040)
-            side2.wait_stream(main)
-            with torch.cuda.stream(side2):
-                ss = self.atten_scale[i][0].run(SS.ch(0, ci))
-                cs = self.cc_scale_transforms[i]
-                t = cs[0].run(ss, act=ACT_GELU)
-                t = cs[2].run(t, act=ACT_GELU)
-                sc = cs[4].run(t, out=SC.ch(sw * i, sw * (i + 1)))
-            ms = self.atten_mean[i][0].run(MS.ch(0, ci), out=LR.ch(0, ci))
-            cm = self.cc_mean_transforms[i]
-            t = cm[0].run(ms, act=ACT_GELU)
-            t = cm[2].run(t, act=ACT_GELU)
-            mu = cm[4].run(t, out=MU.ch(sw * i, sw * (i + 1)))
-            main.wait_stream(side2)
-            yq = LR.ch(ci, ci + sw)
-            Fn.gauss_rate(z3.ch(sw * i, sw * (i + 1)), mu, sc, partials, i * nper, yq=yq,
-                          symbols=Act(SYM, sw * i, sw),
-                          likelihood=Act(LIK, sw * i, sw) if LIK is not None else None,
-                          scale_bound=self.gaussian_conditional._scale_bound,
-                          likelihood_bound=self.gaussian_conditional._likelihood_bound)
-            lr = self.lrp_transforms[i]
-            t = lr[0].run(LR.ch(0, ci + sw), act=ACT_GELU)
-            t = lr[2].run(t, act=ACT_GELU)
-            y2 = SS.ch(192 + sw * i, 192 + sw * (i + 1)) if (not self._shared_support and i < ns - 1) else None
-            lr[4].run(t, out=MS.ch(192 + sw * i, 192 + sw * (i + 1)), epi=EPI_HALF_TANH, r2=yq, y2=y2)
+        self._slice_loop(z3, MS, SS, LR, MU, SC, SYM, LIK, partials, nper)
         y_hat = MS.ch(192, 384)
         x_tilde = self.s_model.run(y_hat)                          # net_ga.py:1078
         main.wait_stream(side)                                     # syntax head joined

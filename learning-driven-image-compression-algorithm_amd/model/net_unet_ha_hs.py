@@ -21,6 +21,7 @@ class Net(_NetGA):
     arch = "net_unet_ha_hs"
     _eb_channels = 512
     _shared_support = True
+    _codable = False   # h_s reads encoder-side features: no decodable bitstream
 
     def _build_hyper(self):
         self.h_a = Unet_ha_new(192, 8, 3)

@@ -10,7 +10,7 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 def _declared():
     txt = (ROOT / "include" / "lic.h").read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(lic_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(lic_\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_header_declares_expected_entry_points():
@@ -40,3 +40,32 @@ def test_ctypes_struct_layout_matches_header():
     body = hdr[hdr.index("typedef struct lic_conv_args"):hdr.index("} lic_conv_args;")]
     for n in names:
         assert re.search(r"\b%s\b" % n, body), n
+
+
+def test_ctypes_struct_offsets_match_c_compiler(tmp_path):
+    """Every args struct of include/lic.h: sizeof and each field's offsetof from gcc
+    equal the ctypes layout (the ABI the Python host passes by pointer)."""
+    import ctypes
+    import shutil
+    import subprocess
+    import pytest
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    structs = {"lic_conv_args": _ffi.ConvArgs, "lic_attn_args": _ffi.AttnArgs,
+               "lic_rate_args": _ffi.RateArgs, "lic_rans_args": _ffi.RansArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lic.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
+        for f in py._fields_:
+            assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])

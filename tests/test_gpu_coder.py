@@ -1,0 +1,213 @@
+"""GPU: the HIP entropy coder (csrc/rans.hip via lic_amd.entropy_coder) against the CPU
+oracle (oracle/ref_coder.py + oracle/rans_ref.c, compressai 1.2.x restated; parity
+with compressai itself unpinned).
+
+Bars: integer work bit-exact — CDF quantisation given the pmf, build_indexes, every
+stream's words, decoded symbols; pmf values (fp32 erfc / MLP) within 2e-6 abs;
+Net.compress -> decompress reproduces forward()'s symbols and reconstruction bitwise."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_coder as C
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ec():
+    from lic_amd import entropy_coder as EC
+    return EC
+
+
+def _gauss_gpu():
+    EC = _ec()
+    st = C.get_scale_table()
+    tab = EC.gauss_tables(st.to(DEV)).check()
+    return st, tab
+
+
+def test_gauss_tables_match_oracle():
+    EC = _ec()
+    st, tab = _gauss_gpu()
+    pmf, tail, length, center = C.gauss_pmfs(st)
+    cdf_ref, sizes_ref, offs_ref = C.tables_from_pmf(pmf, tail, length, -center)
+    assert tab.sizes.cpu().numpy().tolist() == sizes_ref.tolist()
+    assert tab.offsets.cpu().numpy().tolist() == offs_ref.tolist()
+    # pmf (fp32 erfc): tolerance; quantisation of the GPU's own pmf: bit-exact
+    T, stride = tab.cdf.shape
+    gpmf = torch.zeros((T, stride - 1), dtype=torch.float32, device=DEV)
+    from lic_amd.functional import _dp, _lib, stream_handle
+    cen = center.to(DEV).contiguous()
+    assert _lib().lic_gauss_pmf(_dp(st.to(DEV).contiguous()), _dp(cen), T, stride - 1, _dp(gpmf),
+                                stream_handle()) == 0
+    gp = gpmf.cpu()
+    for t in range(T):
+        L = int(length[t])
+        torch.testing.assert_close(gp[t, :L], pmf[t, :L], rtol=0, atol=2e-6)
+        torch.testing.assert_close(gp[t, L:L + 1], tail[t], rtol=1e-4, atol=1e-12)
+        q = C.pmf_to_quantized_cdf(gp[t, :L + 1].tolist())
+        assert (tab.cdf[t, :L + 2].cpu().numpy() == q).all(), t
+    # the oracle's own pmf (torch CPU erfc) differs from the GPU's by ulps; a flipped
+    # rounding moves the renormalised cumulative counts by a few units of 2^-16
+    d = np.abs(tab.cdf.cpu().numpy().astype(np.int64) - cdf_ref.astype(np.int64))
+    print(f"\n[gauss tables] entries differing from the oracle's own pmf path: {int((d > 0).sum())} "
+          f"of {int(sizes_ref.sum())}, max |diff| {int(d.max())} / 65536")
+    assert int(d.max()) <= 256
+
+
+def test_eb_tables_match_oracle():
+    EC = _ec()
+    from lic_amd.layers.compressai import EntropyBottleneck
+    torch.manual_seed(5)
+    eb = EntropyBottleneck(16)
+    with torch.no_grad():  # trained-looking parameters: spread quantiles, non-zero factors
+        for n, p in eb.named_parameters():
+            p.add_(torch.randn_like(p) * 0.3)
+        eb.quantiles[:, 0, 0] = -torch.rand(16) * 20 - 1
+        eb.quantiles[:, 0, 2] = torch.rand(16) * 20 + 1
+        eb.quantiles[:, 0, 1] = torch.randn(16) * 0.5
+    P = {"entropy_bottleneck." + k: v.detach().clone() for k, v in eb.named_parameters()}
+    cdf_ref, sizes_ref, offs_ref, med_ref = C.eb_tables(P)
+    tab, med = EC.eb_tables(eb.to(DEV))
+    tab.check()
+    assert tab.sizes.cpu().numpy().tolist() == sizes_ref.tolist()
+    assert tab.offsets.cpu().numpy().tolist() == offs_ref.tolist()
+    assert torch.equal(med.cpu(), med_ref)
+    d = np.abs(tab.cdf.cpu().numpy()[:, :cdf_ref.shape[1]].astype(np.int64) - cdf_ref.astype(np.int64))
+    print(f"\n[eb tables] entries differing from the oracle: {int((d > 0).sum())} of {int(sizes_ref.sum())}, "
+          f"max |diff| {int(d.max())} / 65536")
+    assert int(d.max()) <= 256
+    # quantisation of the GPU's own pmf: bit-exact
+    from lic_amd.functional import _dp, _lib, stream_handle
+    q = eb.quantiles.detach().cpu()
+    minima = torch.clamp(torch.ceil(q[:, 0, 1] - q[:, 0, 0]).int(), min=0)
+    maxima = torch.clamp(torch.ceil(q[:, 0, 2] - q[:, 0, 1]).int(), min=0)
+    length = minima + maxima + 1
+    stride = int(length.max()) + 1
+    params = torch.cat([getattr(eb, n).detach().float().reshape(16, -1) for n in EC._EB_ORDER], 1).contiguous()
+    gpmf = torch.zeros((16, stride), device=DEV)
+    assert _lib().lic_eb_pmf(_dp(params), _dp((q[:, 0, 1] - minima).to(DEV).contiguous()),
+                             _dp(length.to(DEV).contiguous()), 16, stride, _dp(gpmf), stream_handle()) == 0
+    pmf_ref, tail_ref, _, _, _ = C.eb_pmfs(P)
+    gp = gpmf.cpu()
+    for t in range(16):
+        L = int(length[t])
+        torch.testing.assert_close(gp[t, :L], pmf_ref[t, :L], rtol=0, atol=2e-6)
+        torch.testing.assert_close(gp[t, L:L + 1], tail_ref[t], rtol=1e-4, atol=1e-9)
+        assert (tab.cdf[t, :L + 2].cpu().numpy() == C.pmf_to_quantized_cdf(gp[t, :L + 1].tolist())).all(), t
+
+
+def test_gauss_indexes_bit_exact():
+    EC = _ec()
+    from lic_amd.functional import Act
+    st = C.get_scale_table()
+    g = torch.Generator().manual_seed(0)
+    sc = torch.exp(torch.randn(2, 8, 8, 48, generator=g) * 2)
+    sc[0, 0, 0, :8] = torch.cat([st[:4], torch.tensor([0.0, 0.11, 256.0, 1e6])])
+    out = torch.empty(2, 8, 8, 48, dtype=torch.int32, device=DEV)
+    EC.gauss_indexes(Act(sc.to(DEV)), st.to(DEV), 0.11, Act(out))
+    assert torch.equal(out.cpu(), C.build_indexes(sc, st))
+
+
+def _random_latent(B, H, W, Cn, seed):
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, 64, (B, H, W, Cn)).astype(np.int32)
+    sym = np.round(rng.normal(0, 1, idx.shape) * np.exp(idx / 12.0)).astype(np.int32)
+    flat = sym.reshape(-1)
+    flat[::53] = rng.integers(-(1 << 22), 1 << 22, len(flat[::53]))   # bypass-coded values
+    flat[min(7, flat.size - 1)] = 2 ** 30
+    return sym, idx
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 8, 48), (3, 5, 7, 16), (1, 1, 1, 4)])
+def test_encode_bit_exact_and_decode_round_trip(shape):
+    EC = _ec()
+    from lic_amd.functional import Act
+    st, tab = _gauss_gpu()
+    cdf, sizes, offs = C.gauss_tables(st)
+    sym, idx = _random_latent(*shape, seed=sum(shape))
+    words, offsets = EC.encode_streams(Act(torch.from_numpy(sym).to(DEV)), Act(torch.from_numpy(idx).to(DEV)), tab)
+    ref_w, ref_off = C.encode_latent(sym, idx, tab.cdf.cpu().numpy(), sizes, offs)
+    got_off = offsets.cpu().numpy().astype(np.uint32)
+    assert (got_off == ref_off).all()
+    assert (words[:int(got_off[-1])].cpu().numpy().view(np.uint32) == ref_w).all()
+    B, H, W, Cn = shape
+    mu = torch.randn(B, H, W, Cn)
+    out_sym = torch.empty(B, H, W, Cn, dtype=torch.int32, device=DEV)
+    yq = torch.empty(B, H, W, Cn, device=DEV)
+    status = torch.ones(B * Cn, dtype=torch.int32, device=DEV)
+    EC.decode_streams(words, offsets, tab, B, H * W, Cn, 0, Cn, idx=Act(torch.from_numpy(idx).to(DEV)),
+                      yq=Act(yq), mu=Act(mu.to(DEV)), symbols=Act(out_sym), status=status)
+    assert int(status.sum()) == 0
+    assert (out_sym.cpu().numpy() == sym).all()
+    assert torch.equal(yq.cpu(), torch.from_numpy(sym).float() + mu)
+
+
+def test_decode_channel_window_and_strings():
+    """Decode one slice's channel window from per-image strings (the decompress path)."""
+    EC = _ec()
+    from lic_amd.functional import Act
+    st, tab = _gauss_gpu()
+    sym, idx = _random_latent(2, 4, 4, 192, seed=9)
+    words, offsets = EC.encode_streams(Act(torch.from_numpy(sym).to(DEV)), Act(torch.from_numpy(idx).to(DEV)), tab)
+    strings = EC.to_strings(words, offsets, 2, 192)
+    w2, o2 = EC.from_strings(strings, 192, DEV)
+    for i in range(4):
+        out = torch.empty(2, 4, 4, 48, dtype=torch.int32, device=DEV)
+        idx_w = torch.from_numpy(np.ascontiguousarray(idx[..., 48 * i:48 * (i + 1)])).to(DEV)
+        EC.decode_streams(w2, o2, tab, 2, 16, 192, 48 * i, 48, idx=Act(idx_w), symbols=Act(out))
+        assert (out.cpu().numpy() == sym[..., 48 * i:48 * (i + 1)]).all()
+
+
+def test_truncated_stream_is_flagged_not_fatal():
+    """A stream cut short is detected (reads stop at its end) instead of faulting."""
+    EC = _ec()
+    from lic_amd.functional import Act
+    st, tab = _gauss_gpu()
+    sym = np.full((1, 8, 8, 1), 40, dtype=np.int32)
+    idx = np.full((1, 8, 8, 1), 5, dtype=np.int32)      # narrow table: every symbol bypass-coded
+    words, offsets = EC.encode_streams(Act(torch.from_numpy(sym).to(DEV)), Act(torch.from_numpy(idx).to(DEV)), tab)
+    n = int(offsets[1])
+    assert n > 4
+    for k in (0, 1, 2, n // 2):
+        status = torch.zeros(1, dtype=torch.int32, device=DEV)
+        out = torch.empty(1, 8, 8, 1, dtype=torch.int32, device=DEV)
+        cut = torch.tensor([0, k], dtype=torch.int32, device=DEV)
+        EC.decode_streams(words, cut, tab, 1, 64, 1, 0, 1, idx=Act(torch.from_numpy(idx).to(DEV)),
+                          symbols=Act(out), status=status)
+        assert int(status[0]) == 1, k
+    status = torch.ones(1, dtype=torch.int32, device=DEV)
+    out = torch.empty(1, 8, 8, 1, dtype=torch.int32, device=DEV)
+    EC.decode_streams(words, offsets, tab, 1, 64, 1, 0, 1, idx=Act(torch.from_numpy(idx).to(DEV)),
+                      symbols=Act(out), status=status)
+    assert int(status[0]) == 0 and (out.cpu().numpy() == sym).all()
+    with pytest.raises(ValueError):
+        EC.from_strings([EC.to_strings(words, offsets, 1, 1)[0][:-4]], 1, DEV)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_net_compress_decompress_round_trip(precision):
+    from lic_amd.model import net_ga
+    torch.manual_seed(0)
+    net = net_ga.Net((2, 256, 256, 3), (2, 256, 256, 3), False, False, precision=precision).to(DEV)
+    x = (torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(4)) * 2 - 1).to(DEV)
+    bpp, v_mse, v_psnr = net(x, "test", return_intermediates=True)
+    fwd_sym = net.last["symbols"].permute(0, 2, 3, 1).cpu()
+    fwd_rec = net.last["x_rec"].cpu()
+    enc = net.compress(x)
+    assert torch.equal(enc["symbols"].cpu(), fwd_sym)
+    dec = net.decompress(enc["strings"], enc["shape"], enc["syntax"])
+    assert torch.equal(dec["symbols"].cpu(), fwd_sym)
+    assert torch.equal(dec["x_hat"].cpu(), fwd_rec)
+    nbits = 8 * sum(len(s) for lst in enc["strings"] for s in lst)
+    bpp_real = nbits / (2 * 256 * 256)
+    print(f"\n[{precision}] estimated y bpp {bpp.item():.4f}, coded (y+z, incl. headers) {bpp_real:.4f}")
+    assert bpp_real > 0.9 * bpp.item()
+
+
+def test_unet_ha_hs_is_not_codable():
+    from lic_amd.model import net_unet_ha_hs
+    net = net_unet_ha_hs.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False).to(DEV)
+    with pytest.raises(NotImplementedError):
+        net.compress(torch.zeros(1, 3, 256, 256, device=DEV))
