@@ -477,14 +477,15 @@ class Net(nn.Module):
     def dtype(self):
         return torch.float16 if self.precision == "fp16" else torch.float32
 
-    def _slice_buffers(self, B, hh, ww, dt, dev):
+    def _slice_buffers(self, B, hh, ww, dt, dev, with_partials: bool = True):
         sw = 192 // self.num_slices
         LR = Act.empty(B, hh, ww, 192 + sw * 4, dt, dev)           # lrp_support (widest: 384)
         MU = Act.empty(B, hh, ww, 192, dt, dev)
         SC = Act.empty(B, hh, ww, 192, dt, dev)
         SYM = torch.empty((B, hh, ww, 192), dtype=torch.int32, device=dev)
         nper = -(-(B * hh * ww * sw) // 256)
-        partials = torch.empty((self.num_slices * nper,), dtype=torch.float64, device=dev)
+        partials = (torch.empty((self.num_slices * nper,), dtype=torch.float64, device=dev)
+                    if with_partials else None)
         return LR, MU, SC, SYM, partials, nper
 
     def _slice_loop(self, z3: Optional[Act], MS: Act, SS: Act, LR: Act, MU: Act, SC: Act, SYM: torch.Tensor,
@@ -633,6 +634,40 @@ class Net(nn.Module):
         Fn.syntax_recon(x_tilde, cw, zeros, x_rec, sq_parts, ppi)
         return {"x_hat": x_rec, "symbols": SYM}
 
+    def _forward_body(self, x_in: torch.Tensor, x_rec: torch.Tensor, partials: torch.Tensor, nper: int,
+                      sq_parts: torch.Tensor, ppi: int, return_intermediates: bool):
+        """encode -> quantize -> decode of a batch on the current stream (+ side streams);
+        writes x_rec, the rate partials and the per-image squared-error partials."""
+        B, _, H, W = x_in.shape
+        dev, dt = x_in.device, self.dtype
+        x = Act.from_nchw(x_in, dt, pad16=True)                   # 3 -> 16-byte zero-padded pixels
+        z3 = self.a_model.run(x)                                  # net_ga.py:988
+        hh, ww = z3.H, z3.W
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+        # syntax head (net_ga.py:1010-1016, :1083) only meets the main chain at the
+        # reconstruction: it runs concurrently on a side stream (joined below)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            syn_r = self.syntax_model.run(z3.ch(0, self.M))
+            cw = self.conv_weights_gen.run(syn_r)
+        # concat buffers: MS = [latent_means | y_hat_0..3], SS = [latent_scales | y_hat_0..2]
+        MS = Act.empty(B, hh, ww, 192 + 192, dt, dev)
+        SS = MS if self._shared_support else Act.empty(B, hh, ww, 192 + 144, dt, dev)
+        z, z_hat = self._hyper(z3, MS.ch(0, 192), SS.ch(0, 192))
+        LR, MU, SC, SYM, _, _ = self._slice_buffers(B, hh, ww, dt, dev, with_partials=False)
+        LIK = torch.empty((B, hh, ww, 192), dtype=torch.float32, device=dev) if return_intermediates else None
+        self._slice_loop(z3, MS, SS, LR, MU, SC, SYM, LIK, partials, nper)
+        y_hat = MS.ch(192, 384)
+        x_tilde = self.s_model.run(y_hat)                          # net_ga.py:1078
+        main.wait_stream(side)                                     # syntax head joined
+        Fn.syntax_recon(x_tilde, cw, x_in, x_rec, sq_parts, ppi)   # :1089-1092, :1118, :1137-1141
+        if return_intermediates:
+            self.last = dict(z3=z3.nchw(), z=z.nchw(), z_hat=z_hat.nchw(), latent_means=MS.ch(0, 192).nchw(),
+                             latent_scales=SS.ch(0, 192).nchw(), y_hat=y_hat.nchw(), means=MU.nchw(),
+                             scales=SC.nchw(), symbols=SYM.permute(0, 3, 1, 2), likelihoods=LIK.permute(0, 3, 1, 2),
+                             x_tilde=x_tilde.nchw(), x_rec=x_rec, syntax=syn_r.nchw())
+
     # ---- forward
     @torch.no_grad()
     def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False):
@@ -646,42 +681,20 @@ class Net(nn.Module):
         b, h, w, c = self.train_size
         x_in = inputs.contiguous().float()
         B, _, H, W = x_in.shape
-        dev, dt = x_in.device, self.dtype
-        x = Act.from_nchw(x_in, dt, pad16=True)                   # 3 -> 16-byte zero-padded pixels
-        z3 = self.a_model.run(x)                                  # net_ga.py:988
-        hh, ww = z3.H, z3.W
-        ns, sw = self.num_slices, 192 // self.num_slices
-        main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev)
-        # syntax head (net_ga.py:1010-1016, :1083) only meets the main chain at the
-        # reconstruction: it runs concurrently on a side stream (joined below)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            syn_r = self.syntax_model.run(z3.ch(0, self.M))
-            cw = self.conv_weights_gen.run(syn_r)
-        # concat buffers: MS = [latent_means | y_hat_0..3], SS = [latent_scales | y_hat_0..2]
-        MS = Act.empty(B, hh, ww, 192 + 192, dt, dev)
-        SS = MS if self._shared_support else Act.empty(B, hh, ww, 192 + 144, dt, dev)
-        z, z_hat = self._hyper(z3, MS.ch(0, 192), SS.ch(0, 192))
-        LR, MU, SC, SYM, partials, nper = self._slice_buffers(B, hh, ww, dt, dev)
-        LIK = torch.empty((B, hh, ww, 192), dtype=torch.float32, device=dev) if return_intermediates else None
-        self._slice_loop(z3, MS, SS, LR, MU, SC, SYM, LIK, partials, nper)
-        y_hat = MS.ch(192, 384)
-        x_tilde = self.s_model.run(y_hat)                          # net_ga.py:1078
-        main.wait_stream(side)                                     # syntax head joined
-        x_rec = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
+        if H % 64 or W % 64:
+            raise ValueError("Net.forward: H and W must be multiples of 64 (eval_net.pad64 pads the image)")
+        dev = x_in.device
+        hh, ww = H // 16, W // 16
+        nper = -(-(B * hh * ww * (192 // self.num_slices)) // 256)
+        partials = torch.empty((self.num_slices * nper,), dtype=torch.float64, device=dev)
         ppi = max(1, min(64, -(-(H * W) // 4096)))
         sq_parts = torch.empty((B * ppi,), dtype=torch.float64, device=dev)
-        Fn.syntax_recon(x_tilde, cw, x_in, x_rec, sq_parts, ppi)   # :1089-1092, :1118, :1137-1141
+        x_rec = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
+        self._forward_body(x_in, x_rec, partials, nper, sq_parts, ppi, return_intermediates)
         num_pixels = B * h * w
         bpp = torch.empty((1,), dtype=torch.float32, device=dev)
-        Fn.bpp_finalize(partials, ns * nper, num_pixels, bpp)      # :1134
+        Fn.bpp_finalize(partials, self.num_slices * nper, num_pixels, bpp)  # :1134
         v_mse = torch.empty((B,), dtype=torch.float32, device=dev)
         v_psnr = torch.empty((1,), dtype=torch.float32, device=dev)
         Fn.psnr_finalize(sq_parts, B, ppi, 3.0 * H * W, v_mse, v_psnr)
-        if return_intermediates:
-            self.last = dict(z3=z3.nchw(), z=z.nchw(), z_hat=z_hat.nchw(), latent_means=MS.ch(0, 192).nchw(),
-                             latent_scales=SS.ch(0, 192).nchw(), y_hat=y_hat.nchw(), means=MU.nchw(),
-                             scales=SC.nchw(), symbols=SYM.permute(0, 3, 1, 2), likelihoods=LIK.permute(0, 3, 1, 2),
-                             x_tilde=x_tilde.nchw(), x_rec=x_rec, syntax=syn_r.nchw())
         return bpp[0], v_mse, v_psnr[0]
