@@ -56,11 +56,11 @@ def _pmc_traffic(dtype, batch, size):
         return None
 
 
-def build_net(arch, precision, size, batch, device, seed=0):
+def build_net(arch, precision, size, batch, device, seed=0, post_processing=False):
     from lic_amd.model import net_ga, net_unet_ha_hs
     torch.manual_seed(seed)
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
-    net = mod.Net((batch, size, size, 3), (batch, size, size, 3), False, False, precision=precision)
+    net = mod.Net((batch, size, size, 3), (batch, size, size, 3), False, post_processing, precision=precision)
     return net
 
 
@@ -156,6 +156,7 @@ def main():
     ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     ap.add_argument("--no-extras", action="store_true", help="skip cpu baseline / parity / fp32 legs")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--post-processing", action="store_true", help="HAN post-processing head (eval_net flag)")
     ap.add_argument("--profile", action="store_true",
                     help="only warm-up + timed replays (for rocprofv3 per-forward kernel breakdowns)")
     args = ap.parse_args()
@@ -166,7 +167,8 @@ def main():
     device = torch.device("cuda", local)
     dtype = torch.float16 if args.precision == "fp16" else torch.float32
 
-    net = build_net(args.arch, args.precision, args.size, args.batch, "cpu", seed=0).to(device)
+    net = build_net(args.arch, args.precision, args.size, args.batch, "cpu", seed=0,
+                    post_processing=args.post_processing).to(device)
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     x = (torch.rand(args.batch, 3, args.size, args.size, generator=g) * 2 - 1).to(device)
 
@@ -221,7 +223,8 @@ def main():
             "dtype": "f16" if dtype == torch.float16 else "f32",
             "data": "synthetic (seeded uniform [-1,1) images, seeded reference-init weights; no checkpoints exist)",
             "config": {"workload": f"{args.arch} Net.forward(x,'test') encode->quantize->decode, "
-                                   f"{args.size}x{args.size}, batch {args.batch} per GPU, hipGraph replay",
+                                   f"{args.size}x{args.size}, batch {args.batch} per GPU, hipGraph replay"
+                                   + (", +HAN post-processing" if args.post_processing else ""),
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"image-sharded x{world} (independent batches, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

@@ -89,8 +89,10 @@ def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=Fals
         device = torch.device("cuda", local)
     mine = D.shard(synthetic_kodak(), rank, world)
     summaries, total_time = [], 0.0
+    keep = []  # every (net, graph) stays alive until the sweep ends (no graph teardown mid-sweep)
     for li, lmbda in enumerate(lambdas):
         nets, graphs = {}, {}
+        keep.append((nets, graphs))
         sums = [0.0, 0.0, 0.0, 0.0]  # bpp, psnr, mse, rd
         for name, img in mine:
             _, h, w = img.shape
@@ -141,6 +143,10 @@ def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=Fals
     # elapsed = slowest rank's forward time; images = all ranks' images over the sweep
     elapsed = D.max_over_ranks(total_time, world, device)
     n_img = len(lambdas) * 24
+    torch.cuda.synchronize()
+    for nets, graphs in keep:   # graphs before the nets whose buffers they replay
+        graphs.clear()
+    keep.clear()
     D.finish(world)
     return summaries, n_img / elapsed, world
 

@@ -273,6 +273,42 @@ int lic_rans_pack(const uint32_t* scratch, int32_t cap, const int32_t* lengths, 
                   uint32_t* offsets_w, uint32_t* out, lic_stream_t stream);
 int lic_rans_decode(const lic_rans_args* a, lic_stream_t stream);
 
+/* ---- HAN post-processing (model/han.py, net_ga.py:1096-1100).
+ * The 3x3 / 1x1 convolutions of HAN run on lic_conv2d_fwd; these are the glue ops.  */
+
+/* CALayer + RCAB residual (han.py:97-113, :205-225):
+ *   y = sigmoid(W2 relu(W1 pooled[b] + b1) + b2);  out = r * y + x
+ * pooled: [n][ldp] dtype (lic_avgpool of r); W1 [cr][c], W2 [c][cr] fp32. */
+int lic_ca_apply_fwd(int32_t dtype, const void* r, int32_t ldr, const void* x, int32_t ldx, int32_t n,
+                     int32_t hw, int32_t c, const void* pooled, int32_t ldp, const float* w1,
+                     const float* b1, const float* w2, const float* b2, int32_t cr, void* out,
+                     int32_t ldo, lic_stream_t stream);
+
+/* LAM_Module (han.py:124-150) over x = ngroups channel windows of c channels
+ * (the NHWC image of the B x N x C x H x W stack):
+ *   E = per-image Gram (fp64 partial sums), A = softmax(max(E) - E),
+ *   out_n = gamma * sum_m A[n][m] x_m + x_n.
+ * parts: n * lic_lam_parts(ngroups) doubles of scratch.  ngroups in {2, 5, 7}. */
+int32_t lic_lam_parts(int32_t ngroups);
+int lic_lam_fwd(int32_t dtype, const void* x, int32_t ldx, int32_t n, int32_t hw, int32_t ngroups,
+                int32_t c, double* parts, const float* gamma, void* out, int32_t ldo, lic_stream_t stream);
+
+/* CSAM_Module (han.py:152-188): out = x * (gamma * sigmoid(conv3d(x) + bias)) + x with
+ * the 3x3x3 Conv3d(1,1,3,1,1) sliding over (channel, y, x); params = {w[27], bias, gamma}. */
+int lic_csam_fwd(int32_t dtype, const void* x, int32_t ldx, int32_t n, int32_t h, int32_t w, int32_t c,
+                 const float* params, void* out, int32_t ldo, lic_stream_t stream);
+
+/* Generalised reconstruction head (net_ga.py:969-979 batch_conv, :1092 tanh,
+ * :1096-1100 HAN tail with add_mean, :1118/:1137-1141 metrics):
+ *   v = W_b xtil (3 x cin per image), mode 1: tanh(v); post (fp32 [12], may be NULL):
+ *   v = P v + p (row-major 3x3 then bias); y (NHWC dtype, ycpad channels, zero padded,
+ *   may be NULL) <- v; x_rec (NCHW fp32, may be NULL) <- clamp(v, -1, 1); with x
+ *   (NCHW fp32 input image) the squared 8-bit errors go to sqerr_partials.        */
+int lic_recon_fwd(int32_t dtype, const void* xtil, int32_t n, int32_t h, int32_t w, int32_t cin,
+                  int32_t ldx, const void* wgen, int32_t ldw, int32_t mode, const float* post,
+                  const float* x, float* x_rec, double* sqerr_partials, int32_t parts_per_img, void* y,
+                  int32_t ldy, int32_t ycpad, lic_stream_t stream);
+
 /* Library info. */
 const char* lic_last_error(void);
 const char* lic_version(void);

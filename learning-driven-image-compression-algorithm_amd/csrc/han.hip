@@ -1,0 +1,361 @@
+// HAN post-processing (reference model/han.py, called at
+// net_ga.py:1096-1100): the non-convolution pieces.  Every 3x3 / 1x1 convolution of
+// HAN runs on the MFMA conv kernels (lic_conv2d_fwd); these kernels are the
+// HBM-bound glue around them:
+//   ca_apply   CALayer + RCAB residual: out = r * sigmoid(W2 relu(W1 avg(r) + b1) + b2) + x
+//   lam_gram / lam_apply   LAM_Module: per-image N x N Gram of the stacked group outputs,
+//              softmax(max - energy), out_n = gamma * sum_m A[n][m] x_m + x_n
+//   csam       CSAM_Module: out = x * (gamma * sigmoid(conv3d_3x3x3(x) + b)) + x, the 3-D
+//              kernel sliding over (channel, y, x) of the NHWC map
+// plus the generalised batch-conv reconstruction (lic_recon_fwd) that closes the path.
+#include "lic_common.h"
+
+namespace lic {
+
+__device__ __forceinline__ double block_sum_f64_256(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];  // valid in every thread
+}
+
+// grid (chunks, n); block 256.  y[c] for this image is recomputed per block (c <= 256,
+// cr <= 32: a few thousand MACs).
+template <typename T>
+__global__ __launch_bounds__(256) void ca_apply_kernel(const T* __restrict__ r, int ldr, const T* __restrict__ x,
+                                                       int ldx, int hw, int c, const T* __restrict__ pooled, int ldp,
+                                                       const float* __restrict__ w1, const float* __restrict__ b1,
+                                                       const float* __restrict__ w2, const float* __restrict__ b2,
+                                                       int cr, T* __restrict__ out, int ldo) {
+  __shared__ float pv[256], hid[32], y[256];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  for (int k = tid; k < c; k += 256) pv[k] = to_f(pooled[(int64_t)b * ldp + k]);
+  __syncthreads();
+  if (tid < cr) {
+    float s = 0.f;
+    for (int k = 0; k < c; ++k) s += w1[tid * c + k] * pv[k];
+    s += b1[tid];
+    hid[tid] = s > 0.f ? s : 0.f;
+  }
+  __syncthreads();
+  for (int k = tid; k < c; k += 256) {
+    float s = 0.f;
+    for (int j = 0; j < cr; ++j) s += w2[k * cr + j] * hid[j];
+    s += b2[k];
+    y[k] = 1.0f / (1.0f + expf(-s));
+  }
+  __syncthreads();
+  const int64_t total = (int64_t)hw * c;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t p = e / c;
+    const int k = (int)(e - p * c);
+    const int64_t pix = (int64_t)b * hw + p;
+    const float v = __fadd_rn(__fmul_rn(to_f(r[pix * ldr + k]), y[k]), to_f(x[pix * ldx + k]));
+    out[pix * ldo + k] = from_f<T>(v);
+  }
+}
+
+// Gram partials: grid (nblk, n); each block sums x_i * x_j (i <= j < N) over its pixel
+// range of one image and all C channels of each group, fp64 per thread.
+template <typename T, int N>
+__global__ __launch_bounds__(256) void lam_gram_kernel(const T* __restrict__ x, int ldx, int hw, int C,
+                                                       double* __restrict__ parts) {
+  __shared__ double red[4];
+  constexpr int NP = N * (N + 1) / 2;
+  const int b = blockIdx.y, tid = threadIdx.x;
+  double acc[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) acc[q] = 0.0;
+  const int64_t total = (int64_t)hw * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t p = e / C;
+    const int k = (int)(e - p * C);
+    const T* px = x + ((int64_t)b * hw + p) * ldx + k;
+    float v[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = to_f(px[i * C]);
+    int q = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int j = i; j < N; ++j) acc[q++] += (double)v[i] * (double)v[j];
+  }
+  double* dst = parts + ((int64_t)b * gridDim.x + blockIdx.x) * NP;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const double t = block_sum_f64_256(acc[q], red);
+    if (tid == 0) dst[q] = t;
+  }
+}
+
+// grid (chunks, n): every block reduces its image's partials (fixed order), forms the
+// attention in LDS and applies it to its pixel range.
+template <typename T, int N>
+__global__ __launch_bounds__(256) void lam_apply_kernel(const T* __restrict__ x, int ldx, int hw, int C,
+                                                        const double* __restrict__ parts, int nblk,
+                                                        const float* __restrict__ gamma, T* __restrict__ out,
+                                                        int ldo) {
+  constexpr int NP = N * (N + 1) / 2;
+  __shared__ float A[N][N];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  if (tid == 0) {
+    double E[N][N];
+    int q = 0;
+    for (int i = 0; i < N; ++i)
+      for (int j = i; j < N; ++j) {
+        double s = 0.0;
+        for (int k = 0; k < nblk; ++k) s += parts[((int64_t)b * nblk + k) * NP + q];
+        E[i][j] = E[j][i] = s;
+        ++q;
+      }
+    for (int i = 0; i < N; ++i) {
+      float en[N];
+      double mx = E[i][0];
+      for (int j = 1; j < N; ++j) mx = E[i][j] > mx ? E[i][j] : mx;
+      for (int j = 0; j < N; ++j) en[j] = (float)(mx - E[i][j]);        // energy_new
+      float m2 = en[0];
+      for (int j = 1; j < N; ++j) m2 = fmaxf(m2, en[j]);
+      float sum = 0.f;
+      for (int j = 0; j < N; ++j) {
+        en[j] = expf(en[j] - m2);
+        sum += en[j];
+      }
+      for (int j = 0; j < N; ++j) A[i][j] = en[j] / sum;
+    }
+  }
+  __syncthreads();
+  const float g = gamma[0];
+  const int64_t total = (int64_t)hw * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t p = e / C;
+    const int k = (int)(e - p * C);
+    const int64_t pix = (int64_t)b * hw + p;
+    const T* px = x + pix * ldx + k;
+    float v[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = to_f(px[i * C]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < N; ++j) s += A[i][j] * v[j];
+      out[pix * ldo + i * C + k] = from_f<T>(__fadd_rn(__fmul_rn(g, s), v[i]));
+    }
+  }
+}
+
+// CSAM: params = {w[kd][kh][kw] (27), bias, gamma}
+template <typename T>
+__global__ __launch_bounds__(256) void csam_kernel(const T* __restrict__ x, int ldx, int n, int h, int w, int C,
+                                                   const float* __restrict__ prm, T* __restrict__ out, int ldo) {
+  __shared__ float wk[29];
+  if (threadIdx.x < 29) wk[threadIdx.x] = prm[threadIdx.x];
+  __syncthreads();
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)n * h * w * C;
+  if (e >= total) return;
+  const int64_t pix = e / C;
+  const int k = (int)(e - pix * C);
+  const int b = (int)(pix / ((int64_t)h * w));
+  const int rem = (int)(pix - (int64_t)b * h * w);
+  const int iy = rem / w, ix = rem - iy * w;
+  float s = 0.f;
+#pragma unroll
+  for (int dd = 0; dd < 3; ++dd) {
+    const int kc = k + dd - 1;
+    if (kc < 0 || kc >= C) continue;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int yy = iy + dy - 1;
+      if (yy < 0 || yy >= h) continue;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int xx = ix + dx - 1;
+        if (xx < 0 || xx >= w) continue;
+        s += wk[dd * 9 + dy * 3 + dx] * to_f(x[(((int64_t)b * h + yy) * w + xx) * ldx + kc]);
+      }
+    }
+  }
+  s += wk[27];
+  const float sg = 1.0f / (1.0f + expf(-s));
+  const float o = __fmul_rn(wk[28], sg);
+  const float xv = to_f(x[pix * ldx + k]);
+  out[pix * ldo + k] = from_f<T>(__fadd_rn(__fmul_rn(xv, o), xv));
+}
+
+// Per-image 1x1 "batch conv" (net_ga.py:969-979) with its finishing steps:
+//   v = sum_c w[b][k][c] xtil[c]  (k < 3);  mode 1: v = tanh(v);  post: v = P v + p (1x1 3->3)
+//   y (NHWC dtype, ycpad channels, zero padded) <- v;  x_rec (NCHW fp32) <- clamp(v, -1, 1)
+//   parts[b][blk] <- sum (round(clamp((x_rec+1)*127.5)) - round((x+1)*127.5))^2   (x != NULL)
+template <typename T>
+__global__ __launch_bounds__(256) void recon_kernel(const T* __restrict__ xtil, int h, int w, int cin, int ldx,
+                                                    int ldw, const T* __restrict__ wgen, int mode,
+                                                    const float* __restrict__ post, const float* __restrict__ x,
+                                                    float* __restrict__ xrec, double* __restrict__ parts,
+                                                    int parts_per_img, T* __restrict__ y, int ldy, int ycpad) {
+  __shared__ double red[4];
+  __shared__ float ws[3 * 64];
+  __shared__ float pm[12];
+  const int b = blockIdx.y;
+  for (int k = threadIdx.x; k < 3 * cin; k += 256) ws[k] = to_f(wgen[(int64_t)b * ldw + k]);
+  if (post && threadIdx.x < 12) pm[threadIdx.x] = post[threadIdx.x];
+  __syncthreads();
+  const int64_t hw = (int64_t)h * w;
+  double acc = 0.0;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < hw; p += (int64_t)parts_per_img * 256) {
+    const T* xp = xtil + ((int64_t)b * hw + p) * ldx;
+    float o[3] = {0.f, 0.f, 0.f};
+    for (int c = 0; c < cin; ++c) {
+      const float v = to_f(xp[c]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) o[k] += ws[k * cin + c] * v;
+    }
+    if (mode == 1) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) o[k] = tanhf(o[k]);
+    }
+    if (post) {
+      float q[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) q[k] = pm[3 * k] * o[0] + pm[3 * k + 1] * o[1] + pm[3 * k + 2] * o[2] + pm[9 + k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) o[k] = q[k];
+    }
+    if (y) {
+      T* yp = y + ((int64_t)b * hw + p) * ldy;
+      for (int k = 0; k < ycpad; ++k) yp[k] = from_f<T>(k < 3 ? o[k] : 0.f);
+    }
+    if (xrec) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float t = fminf(fmaxf(o[k], -1.f), 1.f);
+        const int64_t off = ((int64_t)b * 3 + k) * hw + p;
+        xrec[off] = t;
+        if (x) {
+          const float gt = rintf(__fmul_rn(__fadd_rn(x[off], 1.f), 127.5f));
+          float xh = __fmul_rn(__fadd_rn(t, 1.f), 127.5f);
+          xh = rintf(fminf(fmaxf(xh, 0.f), 255.f));
+          const float d = __fsub_rn(xh, gt);
+          acc += (double)(d * d);
+        }
+      }
+    }
+  }
+  if (x && parts) {
+    const double t = block_sum_f64_256(acc, red);
+    if (threadIdx.x == 0) parts[(int64_t)b * parts_per_img + blockIdx.x] = t;
+  }
+}
+
+static unsigned chunks_for(int64_t total) {
+  int64_t c = (total + 256 * 8 - 1) / (256 * 8);  // ~8 elements per thread
+  if (c < 1) c = 1;
+  if (c > 1024) c = 1024;
+  return (unsigned)c;
+}
+
+}  // namespace lic
+
+using namespace lic;
+
+extern "C" int lic_ca_apply_fwd(int32_t dtype, const void* r, int32_t ldr, const void* x, int32_t ldx, int32_t n,
+                                int32_t hw, int32_t c, const void* pooled, int32_t ldp, const float* w1,
+                                const float* b1, const float* w2, const float* b2, int32_t cr, void* out,
+                                int32_t ldo, lic_stream_t stream) {
+  if (n == 0 || hw == 0) return 0;
+  if (c > 256 || cr > 32 || cr < 1) return fail("ca_apply: needs c <= 256 and 1 <= c/reduction <= 32");
+  dim3 grid(chunks_for((int64_t)hw * c), n);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == LIC_F32)
+    hipLaunchKernelGGL(ca_apply_kernel<float>, grid, dim3(256), 0, s, (const float*)r, ldr, (const float*)x, ldx, hw,
+                       c, (const float*)pooled, ldp, w1, b1, w2, b2, cr, (float*)out, ldo);
+  else if (dtype == LIC_F16)
+    hipLaunchKernelGGL(ca_apply_kernel<half_t>, grid, dim3(256), 0, s, (const half_t*)r, ldr, (const half_t*)x, ldx,
+                       hw, c, (const half_t*)pooled, ldp, w1, b1, w2, b2, cr, (half_t*)out, ldo);
+  else
+    return fail("ca_apply: bad dtype");
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int N>
+static int lam_launch(int32_t dtype, const void* x, int32_t ldx, int32_t n, int32_t hw, int32_t C, double* parts,
+                      int32_t nblk, const float* gamma, void* out, int32_t ldo, hipStream_t s) {
+  dim3 g1(nblk, n), g2(chunks_for((int64_t)hw * C), n);
+  if (dtype == LIC_F32) {
+    hipLaunchKernelGGL((lam_gram_kernel<float, N>), g1, dim3(256), 0, s, (const float*)x, ldx, hw, C, parts);
+    hipLaunchKernelGGL((lam_apply_kernel<float, N>), g2, dim3(256), 0, s, (const float*)x, ldx, hw, C, parts, nblk,
+                       gamma, (float*)out, ldo);
+  } else if (dtype == LIC_F16) {
+    hipLaunchKernelGGL((lam_gram_kernel<half_t, N>), g1, dim3(256), 0, s, (const half_t*)x, ldx, hw, C, parts);
+    hipLaunchKernelGGL((lam_apply_kernel<half_t, N>), g2, dim3(256), 0, s, (const half_t*)x, ldx, hw, C, parts,
+                       nblk, gamma, (half_t*)out, ldo);
+  } else {
+    return fail("lam: bad dtype");
+  }
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int32_t lic_lam_parts(int32_t ngroups) { return 256 * ngroups * (ngroups + 1) / 2; }
+
+extern "C" int lic_lam_fwd(int32_t dtype, const void* x, int32_t ldx, int32_t n, int32_t hw, int32_t ngroups,
+                           int32_t c, double* parts, const float* gamma, void* out, int32_t ldo,
+                           lic_stream_t stream) {
+  if (n == 0 || hw == 0) return 0;
+  if (out == x) return fail("lam: out must not alias x");
+  const int nblk = 256;  // parts must hold n * lic_lam_parts(ngroups) doubles
+  hipStream_t s = (hipStream_t)stream;
+  switch (ngroups) {
+    case 5: return lam_launch<5>(dtype, x, ldx, n, hw, c, parts, nblk, gamma, out, ldo, s);
+    case 7: return lam_launch<7>(dtype, x, ldx, n, hw, c, parts, nblk, gamma, out, ldo, s);
+    case 2: return lam_launch<2>(dtype, x, ldx, n, hw, c, parts, nblk, gamma, out, ldo, s);
+    default: return fail("lam: ngroups must be 5 (HAN), 7 (HAN is_high) or 2");
+  }
+}
+
+extern "C" int lic_csam_fwd(int32_t dtype, const void* x, int32_t ldx, int32_t n, int32_t h, int32_t w, int32_t c,
+                            const float* params, void* out, int32_t ldo, lic_stream_t stream) {
+  const int64_t total = (int64_t)n * h * w * c;
+  if (total == 0) return 0;
+  if (out == x) return fail("csam: out must not alias x");
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == LIC_F32)
+    hipLaunchKernelGGL(csam_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, ldx, n, h, w, c, params,
+                       (float*)out, ldo);
+  else if (dtype == LIC_F16)
+    hipLaunchKernelGGL(csam_kernel<half_t>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, ldx, n, h, w, c, params,
+                       (half_t*)out, ldo);
+  else
+    return fail("csam: bad dtype");
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_recon_fwd(int32_t dtype, const void* xtil, int32_t n, int32_t h, int32_t w, int32_t cin,
+                             int32_t ldx, const void* wgen, int32_t ldw, int32_t mode, const float* post,
+                             const float* x, float* x_rec, double* sqerr_partials, int32_t parts_per_img, void* y,
+                             int32_t ldy, int32_t ycpad, lic_stream_t stream) {
+  if (cin > 64) return fail("recon: cin > 64");
+  if (mode != 0 && mode != 1) return fail("recon: mode must be 0 (linear) or 1 (tanh)");
+  if (y && (ycpad < 3 || ldy < ycpad)) return fail("recon: y needs >= 3 channels");
+  if (x && !x_rec) return fail("recon: metrics need x_rec");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(parts_per_img, n);
+  if (dtype == LIC_F32)
+    hipLaunchKernelGGL(recon_kernel<float>, grid, dim3(256), 0, s, (const float*)xtil, h, w, cin, ldx, ldw,
+                       (const float*)wgen, mode, post, x, x_rec, sqerr_partials, parts_per_img, (float*)y, ldy, ycpad);
+  else if (dtype == LIC_F16)
+    hipLaunchKernelGGL(recon_kernel<half_t>, grid, dim3(256), 0, s, (const half_t*)xtil, h, w, cin, ldx, ldw,
+                       (const half_t*)wgen, mode, post, x, x_rec, sqerr_partials, parts_per_img, (half_t*)y, ldy,
+                       ycpad);
+  else
+    return fail("recon: bad dtype");
+  LIC_CHECK_LAUNCH();
+  return 0;
+}

@@ -450,3 +450,48 @@ def to_nchw_f32(x: Act) -> torch.Tensor:
     check(_lib().lic_nhwc_to_nchw(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.c, x.ld, _dp(out),
                                   stream_handle()))
     return out
+
+
+# --------------------------------------------------------------------------- HAN glue (8(f) rank 3)
+def ca_apply(r: Act, x: Act, pooled: Act, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+             out: Optional[Act] = None) -> Act:
+    """out = r * sigmoid(W2 relu(W1 pooled + b1) + b2) + x (CALayer + RCAB residual)."""
+    if out is None:
+        out = Act.empty(r.B, r.H, r.W, r.c, r.dtype, r.t.device)
+    cr = w1.shape[0]
+    check(_lib().lic_ca_apply_fwd(dtype_id(r.dtype), r.ptr, r.ld, x.ptr, x.ld, r.B, r.H * r.W, r.c, pooled.ptr,
+                                  pooled.ld, _dp(w1), _dp(b1), _dp(w2), _dp(b2), cr, out.ptr, out.ld,
+                                  stream_handle()))
+    return out
+
+
+def lam(x: Act, ngroups: int, gamma: torch.Tensor, out: Optional[Act] = None) -> Act:
+    """LAM_Module over `ngroups` channel windows of x.c // ngroups channels."""
+    C = x.c // ngroups
+    if out is None:
+        out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)
+    parts = torch.empty((x.B * int(_lib().lic_lam_parts(ngroups)),), dtype=torch.float64, device=x.t.device)
+    check(_lib().lic_lam_fwd(dtype_id(x.dtype), x.ptr, x.ld, x.B, x.H * x.W, ngroups, C, _dp(parts), _dp(gamma),
+                             out.ptr, out.ld, stream_handle()))
+    return out
+
+
+def csam(x: Act, params: torch.Tensor, out: Optional[Act] = None) -> Act:
+    """CSAM_Module; params = fp32 [w(27), bias, gamma] on the device."""
+    if out is None:
+        out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)
+    check(_lib().lic_csam_fwd(dtype_id(x.dtype), x.ptr, x.ld, x.B, x.H, x.W, x.c, _dp(params), out.ptr, out.ld,
+                              stream_handle()))
+    return out
+
+
+def recon(xtil: Act, wgen: Act, mode: int, post: Optional[torch.Tensor] = None, x: Optional[torch.Tensor] = None,
+          x_rec: Optional[torch.Tensor] = None, parts: Optional[torch.Tensor] = None, ppi: int = 1,
+          y: Optional[Act] = None):
+    """Batch-conv reconstruction head (lic_recon_fwd): mode 1 = tanh, 0 = linear; post = 1x1 3->3."""
+    B, H, W = xtil.B, xtil.H, xtil.W
+    check(_lib().lic_recon_fwd(dtype_id(xtil.dtype), xtil.ptr, B, H, W, xtil.c, xtil.ld, wgen.ptr, wgen.ld, mode,
+                               _dp(post) if post is not None else None, _dp(x) if x is not None else None,
+                               _dp(x_rec) if x_rec is not None else None, _dp(parts) if parts is not None else None,
+                               ppi, y.ptr if y is not None else None, y.ld if y is not None else 0,
+                               y.zpad if y is not None else 0, stream_handle()))

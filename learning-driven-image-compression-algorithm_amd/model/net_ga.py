@@ -13,7 +13,9 @@ Deviations (documented in DESIGN.md):
     visual_FeatureMap_heat re-runs (:989-990, :1008-1009) are not executed.
   * BlockSample / NeighborSample constant buffers (~425 MB, unused in forward) are not
     materialised; their keys are accepted and ignored by load_state_dict.
-  * post_processing=True (HAN) is not implemented yet (raises).
+  * post_processing=True builds HAN / conv_weights_gen_HAN / add_mean after every other
+    module (model/han.py on liblic); with post_processing=False their checkpoint keys are
+    accepted and ignored, as before.
 """
 from __future__ import annotations
 
@@ -329,8 +331,8 @@ class _Stateless(nn.Module):
     forward path (GaussianModel, NoiseQuant)."""
 
 
-_IGNORED_PREFIXES = ("y_sampler.", "h_sampler.", "test_y_sampler.", "test_h_sampler.", "HAN.",
-                     "conv_weights_gen_HAN.", "add_mean.")
+_HAN_PREFIXES = ("HAN.", "conv_weights_gen_HAN.", "add_mean.")
+_IGNORED_PREFIXES = ("y_sampler.", "h_sampler.", "test_y_sampler.", "test_h_sampler.") + _HAN_PREFIXES
 
 
 class Net(nn.Module):
@@ -393,6 +395,13 @@ class Net(nn.Module):
         self.prediction_model.apply(weight_init)
         self.prediction_model_syntax = PredictionModel_Syntax(in_dim=N, dim=M, outdim=M * 2)
         self.prediction_model_syntax.apply(weight_init)
+        if post_processing:  # net_ga.py:935-940 (built last: the other modules' seeded init is unchanged)
+            from .han import HAN_Head, MeanShift
+            self.HAN = HAN_Head(is_high=self.is_high)
+            self.conv_weights_gen_HAN = conv_generator(in_dim=M, out_dim=64)
+            self.conv_weights_gen_HAN.apply(weight_init)
+            self.add_mean = MeanShift(1.0, (0.4488, 0.4371, 0.4040), (1.0, 1.0, 1.0), 1)
+            self.add_mean.apply(weight_init)
         self.last: Dict[str, torch.Tensor] = {}
 
     # ---- hyper prior (overridden by net_unet_ha_hs)
@@ -453,7 +462,8 @@ class Net(nn.Module):
                                       error_msgs)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
-        sd = {k: v for k, v in state_dict.items() if not k.startswith(_IGNORED_PREFIXES)}
+        ign = tuple(p for p in _IGNORED_PREFIXES if not (self.post_processing and p in _HAN_PREFIXES))
+        sd = {k: v for k, v in state_dict.items() if not k.startswith(ign)}
         return super().load_state_dict(sd, strict=strict, assign=assign)
 
     def base_params(self):
@@ -629,9 +639,7 @@ class Net(nn.Module):
         H, W = hh * 16, ww * 16
         x_rec = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
         ppi = max(1, min(64, -(-(H * W) // 4096)))
-        sq_parts = torch.empty((B * ppi,), dtype=torch.float64, device=dev)
-        zeros = torch.zeros((B, 3, H, W), dtype=torch.float32, device=dev)
-        Fn.syntax_recon(x_tilde, cw, zeros, x_rec, sq_parts, ppi)
+        self._reconstruct(x_tilde, syn, cw, None, x_rec, None, ppi)
         return {"x_hat": x_rec, "symbols": SYM}
 
     def _forward_body(self, x_in: torch.Tensor, x_rec: torch.Tensor, partials: torch.Tensor, nper: int,
@@ -661,18 +669,35 @@ class Net(nn.Module):
         y_hat = MS.ch(192, 384)
         x_tilde = self.s_model.run(y_hat)                          # net_ga.py:1078
         main.wait_stream(side)                                     # syntax head joined
-        Fn.syntax_recon(x_tilde, cw, x_in, x_rec, sq_parts, ppi)   # :1089-1092, :1118, :1137-1141
+        self._reconstruct(x_tilde, syn_r, cw, x_in, x_rec, sq_parts, ppi)
         if return_intermediates:
             self.last = dict(z3=z3.nchw(), z=z.nchw(), z_hat=z_hat.nchw(), latent_means=MS.ch(0, 192).nchw(),
                              latent_scales=SS.ch(0, 192).nchw(), y_hat=y_hat.nchw(), means=MU.nchw(),
                              scales=SC.nchw(), symbols=SYM.permute(0, 3, 1, 2), likelihoods=LIK.permute(0, 3, 1, 2),
                              x_tilde=x_tilde.nchw(), x_rec=x_rec, syntax=syn_r.nchw())
 
+    def _reconstruct(self, x_tilde: Act, syn_r: Act, cw: Act, x_in: Optional[torch.Tensor], x_rec: torch.Tensor,
+                     sq_parts: Optional[torch.Tensor], ppi: int):
+        """net_ga.py:1089-1100 + metrics (:1118, :1137-1141): tanh(batch_conv) and, with
+        post_processing, HAN -> batch_conv(conv_weights_gen_HAN(syntax)) -> add_mean."""
+        if not self.post_processing:
+            Fn.recon(x_tilde, cw, 1, x=x_in, x_rec=x_rec, parts=sq_parts, ppi=ppi)
+            return
+        B, H, W = x_tilde.B, x_tilde.H, x_tilde.W
+        epc = 16 // x_tilde.t.element_size()
+        xbf = Act(torch.empty((B, H, W, epc), dtype=x_tilde.dtype, device=x_tilde.t.device), 0, 3, epc)
+        Fn.recon(x_tilde, cw, 1, y=xbf)                                    # :1089-1092
+        xh = self.HAN.run(xbf)                                             # :1097
+        cwh = self.conv_weights_gen_HAN.run(syn_r)                         # :1098
+        post = self.__dict__.get("_lic_add_mean")
+        if post is None or post[0] != self.add_mean.weight._version:
+            post = (self.add_mean.weight._version, self.add_mean.post_params().to(x_tilde.t.device))
+            self.__dict__["_lic_add_mean"] = post
+        Fn.recon(xh, cwh, 0, post=post[1], x=x_in, x_rec=x_rec, parts=sq_parts, ppi=ppi)   # :1099-1100
+
     # ---- forward
     @torch.no_grad()
     def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False):
-        if self.post_processing:
-            raise NotImplementedError("post_processing (HAN) is not implemented on the HIP path yet")
         if not inputs.is_cuda:
             raise RuntimeError("lic_amd Net runs on the GPU only (HIP path); move inputs to cuda")
         if mode != 'test':

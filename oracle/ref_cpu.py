@@ -563,6 +563,72 @@ def batch_conv(weights: Tensor, inputs: Tensor) -> Tensor:
     return torch.cat(torch.split(out, ch_out, dim=1), dim=0)
 
 
+# --------------------------------------------------------------------------- HAN post-processing (8(f) rank 3)
+def han_ca_layer(x: Tensor, P: Params, pfx: str) -> Tensor:
+    """CALayer.forward, model/han.py:97-113: x * sigmoid(1x1(relu(1x1(avgpool(x)))))."""
+    y = F.adaptive_avg_pool2d(x, 1)
+    y = torch.relu(_conv(y, P, pfx + ".conv_du.0"))
+    y = torch.sigmoid(_conv(y, P, pfx + ".conv_du.2"))
+    return x * y
+
+
+def han_rcab(x: Tensor, P: Params, pfx: str) -> Tensor:
+    """RCAB.forward, model/han.py:205-225 (res_scale unused: res = body(x); res += x)."""
+    r = _conv(torch.relu(_conv(x, P, pfx + ".body.0", 1, 1)), P, pfx + ".body.2", 1, 1)
+    return han_ca_layer(r, P, pfx + ".body.3") + x
+
+
+def han_residual_group(x: Tensor, P: Params, pfx: str, n_resblocks: int) -> Tensor:
+    """ResidualGroup.forward, model/han.py:228-242."""
+    res = x
+    for i in range(n_resblocks):
+        res = han_rcab(res, P, f"{pfx}.body.{i}")
+    res = _conv(res, P, f"{pfx}.body.{n_resblocks}", 1, 1)
+    return res + x
+
+
+def han_lam(x: Tensor, gamma: Tensor) -> Tensor:
+    """LAM_Module.forward, model/han.py:124-150 (x: B x N x C x H x W)."""
+    B, N, C, H, W = x.size()
+    q = x.view(B, N, -1)
+    k = x.view(B, N, -1).permute(0, 2, 1)
+    energy = torch.bmm(q, k)
+    energy_new = torch.max(energy, -1, keepdim=True)[0].expand_as(energy) - energy
+    attention = torch.softmax(energy_new, dim=-1)
+    out = torch.bmm(attention, x.view(B, N, -1)).view(B, N, C, H, W)
+    out = gamma * out + x
+    return out.view(B, -1, H, W)
+
+
+def han_csam(x: Tensor, P: Params, pfx: str) -> Tensor:
+    """CSAM_Module.forward, model/han.py:152-188: x * (gamma * sigmoid(conv3d(x))) + x."""
+    B, C, H, W = x.size()
+    out = torch.sigmoid(F.conv3d(x.unsqueeze(1), P[pfx + ".conv.weight"], P[pfx + ".conv.bias"], 1, 1))
+    out = P[pfx + ".gamma"] * out
+    out = out.view(B, -1, H, W)
+    return x * out + x
+
+
+def han_head(x: Tensor, P: Params, pfx: str = "HAN", is_high: bool = False) -> Tensor:
+    """HAN_Head.forward, model/han.py:247-284."""
+    n_rg, n_rb = (6, 12) if is_high else (4, 8)
+    x = _conv(x, P, pfx + ".sub_mean")
+    x = _conv(x, P, pfx + ".head.0", 1, 1)
+    res = x
+    res1 = None
+    for i in range(n_rg + 1):
+        res = (han_residual_group(res, P, f"{pfx}.body.{i}", n_rb) if i < n_rg
+               else _conv(res, P, f"{pfx}.body.{i}", 1, 1))
+        res1 = res.unsqueeze(1) if res1 is None else torch.cat([res.unsqueeze(1), res1], 1)
+    out1 = res
+    res = han_lam(res1, P[pfx + ".la.gamma"])
+    out2 = _conv(res, P, pfx + ".last_conv", 1, 1)
+    out1 = han_csam(out1, P, pfx + ".csa")
+    out = torch.cat([out1, out2], 1)
+    res = _conv(out, P, pfx + ".last", 1, 1)
+    return res + x
+
+
 # --------------------------------------------------------------------------- full forward
 def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Params, num_slices: int = 4):
     """Channel-conditional slice loop, net_ga.py:1021-1067 (eval / dequantize semantics)."""
@@ -599,7 +665,8 @@ def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Param
 
 
 @torch.no_grad()
-def net_forward(x: Tensor, P: Params, arch: str = "net_ga", train_hw=None, M: int = 16) -> Dict[str, Tensor]:
+def net_forward(x: Tensor, P: Params, arch: str = "net_ga", train_hw=None, M: int = 16,
+                post_processing: bool = False, is_high: bool = False) -> Dict[str, Tensor]:
     """Net.forward(inputs, 'test') for arch in {'net_ga', 'net_unet_ha_hs'}:
     net_ga.py:981-1144 / net_unet_ha_hs.py:868-1032, eval (dequantize) semantics,
     visualisation / PNG side effects omitted.  Returns a dict of intermediates."""
@@ -626,6 +693,10 @@ def net_forward(x: Tensor, P: Params, arch: str = "net_ga", train_hw=None, M: in
     x_tilde = synthesis_transform(y_hat, P)
     cw = conv_generator(syn_r, P, "conv_weights_gen", M)
     x_bf = torch.tanh(batch_conv(cw, x_tilde))
+    if post_processing:                                          # net_ga.py:1096-1100
+        x_p = han_head(x_bf, P, "HAN", is_high)
+        cw_h = conv_generator(syn_r, P, "conv_weights_gen_HAN", 64)
+        x_bf = _conv(batch_conv(cw_h, x_p), P, "add_mean")
     x_t = torch.clamp(x_bf, -1, 1)
     num_pixels = B * h * w
     bpp = torch.sum(torch.log(lik), [0, 1, 2, 3]) / (-np.log(2) * num_pixels)

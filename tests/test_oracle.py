@@ -145,3 +145,20 @@ def test_batch_conv_is_per_image_1x1():
     out = R.batch_conv(w, x)
     ref = torch.einsum("boc,bchw->bohw", w[..., 0, 0], x)
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_han_lam_csam_identity_at_zero_gamma_and_lam_known_answer():
+    """han.py LAM / CSAM with gamma = 0 are identities (default init); LAM on two
+    orthogonal unit maps: energy = I, energy_new = 1 - I, softmax rows = [1, e] / (1 + e)."""
+    import math
+    x = torch.randn(2, 5, 4, 3, 3)
+    assert torch.equal(R.han_lam(x, torch.zeros(1)), x.view(2, 20, 3, 3))
+    P = {"c.conv.weight": torch.randn(1, 1, 3, 3, 3), "c.conv.bias": torch.randn(1), "c.gamma": torch.zeros(1)}
+    y = torch.randn(1, 4, 5, 5)
+    assert torch.equal(R.han_csam(y, P, "c"), y)
+    e0 = torch.zeros(1, 2, 1, 1, 2)
+    e0[0, 0, 0, 0, 0] = 1.0
+    e0[0, 1, 0, 0, 1] = 1.0
+    out = R.han_lam(e0, torch.ones(1)).view(1, 2, 1, 1, 2)
+    a_self, a_other = 1 / (1 + math.e), math.e / (1 + math.e)
+    torch.testing.assert_close(out[0, 0, 0, 0], torch.tensor([1 + a_self, a_other]))
