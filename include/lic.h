@@ -276,11 +276,18 @@ int lic_rans_decode(const lic_rans_args* a, lic_stream_t stream);
 /* ---- HAN post-processing (model/han.py, net_ga.py:1096-1100).
  * The 3x3 / 1x1 convolutions of HAN run on lic_conv2d_fwd; these are the glue ops.  */
 
+/* Per-(image, pixel chunk) channel sums of x (fp32): parts[(b*nchunk + k)*c + ch],
+ * chunk k = pixels [k*ceil(hw/nchunk), ...).  The CALayer average pool in two
+ * passes, so a 256x256 map is reduced by n*nchunk workgroups.                    */
+int lic_pool_partials(int32_t dtype, const void* x, int32_t ldx, int32_t n, int32_t hw, int32_t c,
+                      int32_t nchunk, float* parts, lic_stream_t stream);
+
 /* CALayer + RCAB residual (han.py:97-113, :205-225):
- *   y = sigmoid(W2 relu(W1 pooled[b] + b1) + b2);  out = r * y + x
- * pooled: [n][ldp] dtype (lic_avgpool of r); W1 [cr][c], W2 [c][cr] fp32. */
+ *   y = sigmoid(W2 relu(W1 mean + b1) + b2), mean = sum_k parts[b][k] / hw;  out = r * y + x
+ * parts from lic_pool_partials(r), sized n*(nchunk+1)*c floats: y[b][c] is written after
+ * the partials.  W1 [cr][c], W2 [c][cr] fp32. */
 int lic_ca_apply_fwd(int32_t dtype, const void* r, int32_t ldr, const void* x, int32_t ldx, int32_t n,
-                     int32_t hw, int32_t c, const void* pooled, int32_t ldp, const float* w1,
+                     int32_t hw, int32_t c, float* parts, int32_t nchunk, const float* w1,
                      const float* b1, const float* w2, const float* b2, int32_t cr, void* out,
                      int32_t ldo, lic_stream_t stream);
 
@@ -288,7 +295,8 @@ int lic_ca_apply_fwd(int32_t dtype, const void* r, int32_t ldr, const void* x, i
  * (the NHWC image of the B x N x C x H x W stack):
  *   E = per-image Gram (fp64 partial sums), A = softmax(max(E) - E),
  *   out_n = gamma * sum_m A[n][m] x_m + x_n.
- * parts: n * lic_lam_parts(ngroups) doubles of scratch.  ngroups in {2, 5, 7}. */
+ * parts: n * lic_lam_parts(ngroups) doubles of scratch (Gram partials, then the
+ * per-image attention matrices).  ngroups in {2, 5, 7}. */
 int32_t lic_lam_parts(int32_t ngroups);
 int lic_lam_fwd(int32_t dtype, const void* x, int32_t ldx, int32_t n, int32_t hw, int32_t ngroups,
                 int32_t c, double* parts, const float* gamma, void* out, int32_t ldo, lic_stream_t stream);

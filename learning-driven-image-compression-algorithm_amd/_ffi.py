@@ -26,7 +26,7 @@ EXPORTED_SYMBOLS = (
     "lic_avgpool", "lic_rb3_fwd", "lic_last_error", "lic_version", "lic_device_arch",
     "lic_gauss_pmf", "lic_eb_pmf", "lic_pmf_to_cdf", "lic_gauss_indexes", "lic_quantize_symbols",
     "lic_rans_cap", "lic_rans_encode", "lic_rans_pack", "lic_rans_decode",
-    "lic_ca_apply_fwd", "lic_lam_parts", "lic_lam_fwd", "lic_csam_fwd", "lic_recon_fwd",
+    "lic_pool_partials", "lic_ca_apply_fwd", "lic_lam_parts", "lic_lam_fwd", "lic_csam_fwd", "lic_recon_fwd",
 )
 LIC_EB_PARAMS = 58
 
@@ -153,6 +153,7 @@ def load():
         "lic_rans_encode": [V, V],
         "lic_rans_pack": [V, I, V, I, V, V, V],
         "lic_rans_decode": [V, V],
+        "lic_pool_partials": [I, V, I, I, I, I, I, V, V],
         "lic_ca_apply_fwd": [I, V, I, V, I, I, I, I, V, I, V, V, V, V, I, V, I, V],
         "lic_lam_fwd": [I, V, I, I, I, I, I, V, V, V, I, V],
         "lic_csam_fwd": [I, V, I, I, I, I, I, V, V, I, V],

@@ -36,6 +36,9 @@ static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status
     if constexpr (sizeof(T) == 2) {
       if (HALO_BIG_TILE && a.copad % 192 == 0 && a.isy == 1 && a.isx == 1 && a.mi > 16 && blocks(32, 16, 192) >= 200)
         return try_halo<T, 32, 16, 192, 4, 2>(a, s, status);
+      // 64-channel maps (HAN at full resolution): same tile, one 64-wide channel block
+      if (HALO_BIG_TILE && a.copad == 64 && a.isy == 1 && a.isx == 1 && a.mi > 16 && blocks(32, 16, 64) >= 1024)
+        return try_halo<T, 32, 16, 64, 8, 1>(a, s, status);
     }
     if (a.copad % 192 == 0 && blocks(16, 16, 192) >= 200) return try_halo<T, 16, 16, 192, 4, 2>(a, s, status);
     if (a.copad % 128 == 0 && blocks(16, 16, 128) >= 200) return try_halo<T, 16, 16, 128, 4, 2>(a, s, status);

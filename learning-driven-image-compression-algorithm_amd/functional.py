@@ -453,14 +453,25 @@ def to_nchw_f32(x: Act) -> torch.Tensor:
 
 
 # --------------------------------------------------------------------------- HAN glue (8(f) rank 3)
-def ca_apply(r: Act, x: Act, pooled: Act, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
-             out: Optional[Act] = None) -> Act:
-    """out = r * sigmoid(W2 relu(W1 pooled + b1) + b2) + x (CALayer + RCAB residual)."""
+def pool_partials(x: Act, nchunk: int, parts: torch.Tensor) -> torch.Tensor:
+    """Per-(image, pixel chunk) fp32 channel sums (the first pass of an average pool)."""
+    if parts.numel() < x.B * nchunk * x.c or parts.dtype != torch.float32:
+        raise ValueError("pool_partials: parts must be fp32 with B * nchunk * C entries")
+    check(_lib().lic_pool_partials(dtype_id(x.dtype), x.ptr, x.ld, x.B, x.H * x.W, x.c, nchunk, _dp(parts),
+                                   stream_handle()))
+    return parts
+
+
+def ca_apply(r: Act, x: Act, parts: torch.Tensor, nchunk: int, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
+             b2: torch.Tensor, out: Optional[Act] = None) -> Act:
+    """out = r * sigmoid(W2 relu(W1 mean(r) + b1) + b2) + x (CALayer + RCAB residual)."""
     if out is None:
         out = Act.empty(r.B, r.H, r.W, r.c, r.dtype, r.t.device)
+    if parts.numel() < r.B * (nchunk + 1) * r.c:
+        raise ValueError("ca_apply: parts must hold B * (nchunk + 1) * C floats")
     cr = w1.shape[0]
-    check(_lib().lic_ca_apply_fwd(dtype_id(r.dtype), r.ptr, r.ld, x.ptr, x.ld, r.B, r.H * r.W, r.c, pooled.ptr,
-                                  pooled.ld, _dp(w1), _dp(b1), _dp(w2), _dp(b2), cr, out.ptr, out.ld,
+    check(_lib().lic_ca_apply_fwd(dtype_id(r.dtype), r.ptr, r.ld, x.ptr, x.ld, r.B, r.H * r.W, r.c, _dp(parts),
+                                  nchunk, _dp(w1), _dp(b1), _dp(w2), _dp(b2), cr, out.ptr, out.ld,
                                   stream_handle()))
     return out
 

@@ -71,10 +71,12 @@ class CALayer(nn.Module):
 
     def run(self, r: Act, x: Act, out: Optional[Act] = None) -> Act:
         """r * y + x (the RCAB residual fused)."""
-        pooled = Act.empty(r.B, 1, 1, r.c, r.dtype, r.t.device)
-        Fn.avgpool(r, pooled)
+        # avg_pool in two passes (per-chunk sums, then their sum inside ca_apply)
+        nchunk = max(1, min(64, -(-(r.H * r.W) // 1024)))
+        parts = torch.empty((r.B * (nchunk + 1) * r.c,), dtype=torch.float32, device=r.t.device)
+        Fn.pool_partials(r, nchunk, parts)
         w1, b1, w2, b2 = self._mats()
-        return Fn.ca_apply(r, x, pooled, w1, b1, w2, b2, out)
+        return Fn.ca_apply(r, x, parts, nchunk, w1, b1, w2, b2, out)
 
 
 class RCAB(nn.Module):
@@ -178,7 +180,7 @@ class HAN_Head(nn.Module):
         res = head
         for i, m in enumerate(self.body):
             win = stack.ch((G - 1 - i) * F_, (G - i) * F_)
-            res = m.run(res, win) if i < G - 1 else m.run(res, win)
+            res = m.run(res, win)
         out1 = stack.ch(0, F_)
         lam = self.la.run(stack, G)
         cat = Act.empty(B, H, W, 2 * F_, dt, dev)

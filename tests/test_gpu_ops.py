@@ -330,6 +330,8 @@ def test_loud_failure_on_bad_args():
     (192, 192, 5, 2, (1, 1, 2, 2), 8, 128),   # ZeroPad2d((1,2,1,2)) + conv5x5 s2
     (192, 192, 3, 2, (1, 1, 1, 1), 8, 96),    # RBWS conv1 (stride 2), ragged tiles (96/2=48)
     (96, 96, 3, 1, (1, 1, 1, 1), 16, 50),     # ragged tile edges, BN=128 pad
+    (64, 64, 3, 1, (1, 1, 1, 1), 8, 256),     # HAN conv3x3 @ full res (fp16: 32x16 px x 64 ch tiles)
+    (64, 64, 3, 1, (1, 1, 1, 1), 9, 250),     # same, ragged 32x16 tiles
 ])
 def test_conv_halo_matches_generic(dtype, cin, cout, k, s, pad, B, H):
     """The spatial-tile (halo) kernel and the generic implicit-GEMM kernel agree."""

@@ -62,9 +62,11 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--post-processing", action="store_true")
     args = ap.parse_args()
     import bench
-    net = bench.build_net(args.arch, "fp16", args.size, args.batch, "cpu").to("cuda")
+    net = bench.build_net(args.arch, "fp16", args.size, args.batch, "cpu",
+                          post_processing=args.post_processing).to("cuda")
     x = torch.rand(args.batch, 3, args.size, args.size, device="cuda") * 2 - 1
     with torch.no_grad():
         print("warm-up forward", flush=True)
@@ -72,7 +74,8 @@ def main():
         torch.cuda.synchronize()
         print("profiled forward", flush=True)
         for n in ("conv", "conv_transpose", "gdn", "win_attn", "layernorm", "rb3", "add", "copy", "avgpool",
-                  "quantize_median", "gauss_rate", "syntax_recon", "bpp_finalize", "psnr_finalize"):
+                  "quantize_median", "gauss_rate", "syntax_recon", "bpp_finalize", "psnr_finalize",
+                  "recon", "pool_partials", "ca_apply", "lam", "csam"):
             wrap(n)
         net(x, "test")
         torch.cuda.synchronize()
