@@ -317,6 +317,74 @@ int lic_recon_fwd(int32_t dtype, const void* xtil, int32_t n, int32_t h, int32_t
                   const float* x, float* x_rec, double* sqerr_partials, int32_t parts_per_img, void* y,
                   int32_t ldy, int32_t ycpad, lic_stream_t stream);
 
+/* ------------------------------------------------------------------ training path
+ * Backward of the hot-path layers: the reference's
+ * loss.backward() through Net.forward(x, 'train') — train_net_unet.py:177-200 and the
+ * online encoder finetune eval_net.py:170-179.  Conv dgrad needs no entry point: it is
+ * lic_conv2d_fwd over dz with transposed / tap-mirrored (stride 1) or transposed-conv
+ * phase (stride 2) packed weights (lic_amd/autograd.py).                            */
+
+/* Weight gradient of one conv launch (same tap / lattice form as lic_conv2d_fwd):
+ *   dw[n*s_co + c*s_ci + t*s_tap] (+)= sum_{b,i,j} dz[b, oy0+osy*i, ox0+osx*j, n]
+ *                                        * pro(x[b, i*isy+dy[t], j*isx+dx[t], c])
+ * for n < co_out, c < ci_out (x zero outside the map; pro = identity or square, the
+ * latter for GDN's dGamma = sum dn * x^2).  Replaces F.conv2d's / F.conv_transpose2d's
+ * autograd weight gradient (torch.nn.grad.conv2d_weight) for every nn.Conv2d of
+ * net_ga.py / net_unet_ha_hs.py / the layers/ modules and for GDN gamma (model/gdn.py:85-92,
+ * layers/gdn.py:62-75).  MFMA implicit GEMM, K = output pixels split across
+ * work-groups; fp32 partials in caller workspace (size: lic_conv2d_wgrad_workspace),
+ * deterministic reduce.  ci, co, ldx, ldz multiples of 16 bytes; views 16-B aligned. */
+typedef struct lic_wgrad_args {
+  int32_t dtype;
+  const void* x; int32_t n, h, w, ci, ldx;       /* forward input view                 */
+  const void* dz; int32_t ho, wo, co, ldz;       /* grad at the conv output (pre-act)  */
+  int32_t mi, mj, oy0, ox0, osy, osx, isy, isx;  /* lattice, as lic_conv_args          */
+  int32_t ntaps; int8_t dy[LIC_MAX_TAPS]; int8_t dx[LIC_MAX_TAPS];
+  int32_t prologue;                              /* LIC_PRO_NONE or LIC_PRO_SQUARE     */
+  float* dw; int64_t s_co, s_ci, s_tap;          /* fp32 destination + element strides */
+  int32_t co_out, ci_out, accumulate;
+  float* ws; int64_t ws_bytes;
+} lic_wgrad_args;
+int64_t lic_conv2d_wgrad_workspace(const lic_wgrad_args* a);   /* bytes, -1 on bad args */
+int lic_conv2d_wgrad(const lic_wgrad_args* a, lic_stream_t stream);
+
+/* Per-channel sum over pixels (bias / beta gradients): out[c] (+)= sum_p x[p*ldx + c].
+ * fp32 out; workspace lic_channel_sum_workspace(c) bytes.                          */
+int64_t lic_channel_sum_workspace(int32_t c);
+int lic_channel_sum(int32_t dtype, const void* x, int32_t ldx, int32_t npix, int32_t c, float* ws,
+                    int64_t ws_bytes, float* out, int32_t accumulate, lic_stream_t stream);
+
+/* Activation forward / backward: y = act(z); dz = dy * act'(z) (nn.LeakyReLU,
+ * nn.GELU (erf), nn.ReLU; ROUND is straight-through as ste_round, net_ga.py:713-719). */
+int lic_act_fwd(int32_t dtype, const void* z, int32_t ldz, int32_t npix, int32_t c, int32_t act,
+                float slope, void* y, int32_t ldy, lic_stream_t stream);
+int lic_act_bwd(int32_t dtype, const void* z, int32_t ldz, const void* dy, int32_t lddy, int32_t npix,
+                int32_t c, int32_t act, float slope, void* dz, int32_t lddz, lic_stream_t stream);
+
+/* Gate y = g * sigmoid(a) + r (Win_noShift_Attention, layers/layers.py:105-111):
+ * da = dy*g*s*(1-s), dg = dy*s (dg may be NULL); dr = dy needs no kernel.          */
+int lic_gate_bwd(int32_t dtype, const void* a, int32_t lda, const void* g, int32_t ldg, const void* dy,
+                 int32_t lddy, int32_t npix, int32_t c, void* da, int32_t ldda, void* dg, int32_t lddg,
+                 lic_stream_t stream);
+
+/* GDN / IGDN backward, y = x * n^p, n = beta' + Gamma' x^2 (p = -1/2, +1/2):
+ *   elem:   dxd = dy * n^p,   u = dn = dy * x * p * n^(p-1)
+ *   finish: dx (+)= dxd + 2 x t, with t = Gamma'^T u (lic_conv2d_fwd, transposed pack)
+ * dGamma' = lic_conv2d_wgrad(dz=u, x, PRO_SQUARE), dbeta' = lic_channel_sum(u).
+ * model/gdn.py:69-92 / :133-156, layers/gdn.py:62-75.                              */
+int lic_gdn_bwd_elem(int32_t dtype, const void* x, int32_t ldx, const void* nrm, int32_t ldn,
+                     const void* dy, int32_t lddy, int32_t npix, int32_t c, int32_t inverse, void* dxd,
+                     int32_t lddxd, void* u, int32_t ldu, lic_stream_t stream);
+int lic_gdn_bwd_finish(int32_t dtype, const void* x, int32_t ldx, const void* t, int32_t ldt,
+                       const void* dxd, int32_t lddxd, int32_t npix, int32_t c, void* dx, int32_t lddx,
+                       int32_t accumulate, lic_stream_t stream);
+
+/* LowerBound + square reparametrisation backward (q' = max(q,bound)^2 - pedestal):
+ * dq (+)= [q >= bound or g < 0] * g, g = dq' * 2 max(q, bound).  ops/bound_ops.py:25-28,
+ * model/gdn.py:18-26, ops/parametrizers.py:45-49.  fp32, `count` elements.          */
+int lic_lower_bound_sq_bwd(const float* q, const float* dq_eff, int32_t count, float bound, float* dq,
+                           int32_t accumulate, lic_stream_t stream);
+
 /* Library info. */
 const char* lic_last_error(void);
 const char* lic_version(void);

@@ -1,0 +1,350 @@
+"""Training path, layer level: ``torch.autograd.Function``s whose
+forward AND backward run on liblic.
+
+The reference trains with ``loss.backward()`` through ``Net.forward(x, 'train')``
+(train_net_unet.py:177-200; the online encoder finetune of eval_net.py:170-179 does
+the same through ``a_model``).  Every gradient here is a liblic launch:
+
+* conv dgrad  -> ``lic_conv2d_fwd`` over dz with re-packed weights: stride 1 is the
+  transposed, tap-mirrored conv; stride 2 is four transposed-conv phases (sub-pixel
+  gather form); a ConvTranspose2d's dgrad is the plain strided conv with its weight.
+* conv wgrad  -> ``lic_conv2d_wgrad`` (MFMA implicit GEMM over output pixels).
+* bias / beta -> ``lic_channel_sum``; activations / GDN chain rule / LowerBound ->
+  ``lic_act_bwd``, ``lic_gdn_bwd_elem`` + ``lic_gdn_bwd_finish``,
+  ``lic_lower_bound_sq_bwd``.
+
+Tensors are NHWC ``[B, H, W, C]`` contiguous, fp32 (parity) or fp16; weights are the
+fp32 ``nn.Parameter``s in the reference's layouts (Conv2d ``[co, ci, kh, kw]``,
+ConvTranspose2d ``[ci, co, kh, kw]``, GDN ``beta [C]`` / ``gamma [C, C]``), and their
+gradients come back fp32 in those layouts.  There is no PyTorch compute fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import _ffi
+from . import functional as Fn
+from ._ffi import ACT_NONE, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, PRO_NONE, PRO_SQUARE, WgradArgs, check
+from .functional import Act, ConvPack, _dp, dtype_id, stream_handle
+
+__all__ = ["conv2d", "conv_transpose2d", "gdn", "activation", "wgrad", "channel_sum", "dgrad_packs"]
+
+
+def _lib():
+    return _ffi.load()
+
+
+def _epc(dtype: torch.dtype) -> int:
+    return 16 // torch.empty((), dtype=dtype).element_size()
+
+
+def _pad_channels(t: torch.Tensor) -> torch.Tensor:
+    """NHWC tensor -> contiguous NHWC with C rounded up to 16 bytes (zero channels)."""
+    t = t.contiguous()
+    epc = _epc(t.dtype)
+    C = t.shape[-1]
+    cp = -(-C // epc) * epc
+    if cp == C:
+        return t
+    out = torch.zeros(t.shape[:-1] + (cp,), dtype=t.dtype, device=t.device)
+    out[..., :C] = t
+    return out
+
+
+def _taps(kh, kw, pt, pl):
+    return [ky - pt for ky in range(kh) for kx in range(kw)], [kx - pl for ky in range(kh) for kx in range(kw)]
+
+
+# --------------------------------------------------------------------------- primitives
+def wgrad(x: torch.Tensor, dz: torch.Tensor, dy: Sequence[int], dx: Sequence[int], *, stride: int = 1,
+          lattice: Optional[Tuple[int, int]] = None, dw: torch.Tensor, strides: Tuple[int, int, int],
+          co_out: int, ci_out: int, prologue: int = PRO_NONE, accumulate: bool = False) -> torch.Tensor:
+    """dw[n*s_co + c*s_ci + t*s_tap] (+)= sum_pix dz[pix, n] * pro(x[pix*stride + tap_t, c]).
+    x, dz: NHWC with 16-byte channel counts; lattice = (mi, mj) output pixels (default dz's map)."""
+    if x.dtype != dz.dtype:
+        raise ValueError("wgrad: x and dz dtypes differ")
+    if dw.dtype != torch.float32 or not dw.is_contiguous():
+        raise ValueError("wgrad: dw must be contiguous fp32")
+    B, H, W, ci = x.shape
+    _, Ho, Wo, co = dz.shape
+    mi, mj = lattice if lattice is not None else (Ho, Wo)
+    a = WgradArgs()
+    a.dtype = dtype_id(x.dtype)
+    a.x, a.n, a.h, a.w, a.ci, a.ldx = _dp(x), B, H, W, ci, ci
+    a.dz, a.ho, a.wo, a.co, a.ldz = _dp(dz), Ho, Wo, co, co
+    a.mi, a.mj, a.oy0, a.ox0, a.osy, a.osx, a.isy, a.isx = mi, mj, 0, 0, 1, 1, stride, stride
+    if len(dy) > _ffi.MAX_TAPS:
+        raise ValueError("wgrad: too many taps")
+    a.ntaps = len(dy)
+    for t, (u, v) in enumerate(zip(dy, dx)):
+        a.dy[t], a.dx[t] = u, v
+    a.prologue = prologue
+    a.dw = _dp(dw)
+    a.s_co, a.s_ci, a.s_tap = strides
+    a.co_out, a.ci_out, a.accumulate = co_out, ci_out, 1 if accumulate else 0
+    need = int(_lib().lic_conv2d_wgrad_workspace(ctypes.byref(a)))
+    if need < 0:
+        check(_lib().lic_conv2d_wgrad(ctypes.byref(a), stream_handle()))  # raises with the reason
+    ws = torch.empty((max(need, 4) // 4,), dtype=torch.float32, device=x.device)
+    a.ws, a.ws_bytes = _dp(ws), need
+    check(_lib().lic_conv2d_wgrad(ctypes.byref(a), stream_handle()))
+    return dw
+
+
+def channel_sum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """Per-channel fp32 sum over all pixels of an NHWC tensor (bias gradients)."""
+    x = x.contiguous()
+    C = x.shape[-1]
+    npix = x.numel() // C if C else 0
+    if out is None:
+        out = torch.empty((C,), dtype=torch.float32, device=x.device)
+    ws = torch.empty((int(_lib().lic_channel_sum_workspace(C)) // 4,), dtype=torch.float32, device=x.device)
+    check(_lib().lic_channel_sum(dtype_id(x.dtype), _dp(x), C, npix, C, _dp(ws), ws.numel() * 4, _dp(out),
+                                 1 if accumulate else 0, stream_handle()))
+    return out
+
+
+def _act_fwd(z: torch.Tensor, act: int, slope: float) -> torch.Tensor:
+    C = z.shape[-1]
+    y = torch.empty_like(z)
+    check(_lib().lic_act_fwd(dtype_id(z.dtype), _dp(z), C, z.numel() // C, C, act, slope, _dp(y), C,
+                             stream_handle()))
+    return y
+
+
+def _act_bwd(z: torch.Tensor, dy: torch.Tensor, act: int, slope: float) -> torch.Tensor:
+    C = z.shape[-1]
+    dy = dy.contiguous()
+    dz = torch.empty_like(z)
+    check(_lib().lic_act_bwd(dtype_id(z.dtype), _dp(z), C, _dp(dy), C, z.numel() // C, C, act, slope, _dp(dz), C,
+                             stream_handle()))
+    return dz
+
+
+def dgrad_packs(weight: torch.Tensor, stride: int, pad: Tuple[int, int, int, int], dtype: torch.dtype,
+                co_pad: int):
+    """ConvPacks computing dL/dx of conv2d(x, weight, stride, pad) from dz (co_pad channels) with
+    lic_conv2d_fwd.  stride 1: one pack (weights transposed, taps mirrored); stride s > 1: one
+    pack per output phase (ry, rx) of dx, taps with (r - d) % s == 0 at offset (r - d) // s."""
+    co, ci, kh, kw = weight.shape
+    pt, pl, pb, pr = pad
+    if stride == 1:
+        wt = weight.detach().transpose(0, 1).flip(2, 3)
+        return [Fn.pack_conv2d(wt, None, 1, (kh - 1 - pt, kw - 1 - pl, kh - 1 - pb, kw - 1 - pr), dtype,
+                               cin_to=co_pad)]
+    s = stride
+    packs = []
+    wd = weight.detach()
+    for ry in range(s):
+        for rx in range(s):
+            taps = [(ky, kx) for ky in range(kh) for kx in range(kw)
+                    if (ry - (ky - pt)) % s == 0 and (rx - (kx - pl)) % s == 0]
+            if not taps:
+                continue
+            cpad = Fn._cpad_for(co_pad, dtype)
+            copad = Fn._choose_copad(ci)
+            w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
+            for t, (ky, kx) in enumerate(taps):
+                w[:ci, t, :co] = wd[:, :, ky, kx].t().to(dtype)
+            packs.append(ConvPack(w=w, bias=None, ci=co_pad, co=ci,
+                                  dy=[(ry - (ky - pt)) // s for ky, kx in taps],
+                                  dx=[(rx - (kx - pl)) // s for ky, kx in taps],
+                                  kh=kh, kw=kw, stride=s, phase=(ry, rx, s, s, 0)))
+    return packs
+
+
+def _conv_dgrad(dzp: torch.Tensor, weight: torch.Tensor, stride: int, pad, H: int, W: int) -> torch.Tensor:
+    B = dzp.shape[0]
+    ci = weight.shape[1]
+    packs = dgrad_packs(weight, stride, pad, dzp.dtype, dzp.shape[-1])
+    if stride == 1:
+        return Fn.conv(Act(dzp), packs[0], out_hw=(H, W)).t
+    full = len(packs) == stride * stride
+    dx = (torch.empty if full else torch.zeros)((B, H, W, ci), dtype=dzp.dtype, device=dzp.device)
+    out = Act(dx)
+    for pk in packs:
+        Fn.conv(Act(dzp), pk, out)
+    return dx
+
+
+# --------------------------------------------------------------------------- Conv2d
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, act, slope):
+        co, ci, kh, kw = weight.shape
+        if x.shape[-1] != ci:
+            raise ValueError(f"conv2d: input has {x.shape[-1]} channels, weight expects {ci}")
+        xp = _pad_channels(x)
+        pk = Fn.pack_conv2d(weight, bias, stride, pad, x.dtype, cin_to=xp.shape[-1])
+        z = Fn.conv(Act(xp), pk).t
+        y = _act_fwd(z, act, slope) if act != ACT_NONE else z
+        ctx.save_for_backward(xp, weight, z if act != ACT_NONE else None)
+        ctx.geom = (stride, tuple(pad), act, slope, x.shape[1], x.shape[2], bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xp, weight, z = ctx.saved_tensors
+        stride, pad, act, slope, H, W, has_bias = ctx.geom
+        co, ci, kh, kw = weight.shape
+        dz = _act_bwd(z, dy, act, slope) if act != ACT_NONE else dy.contiguous()
+        dzp = _pad_channels(dz)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_dgrad(dzp, weight, stride, pad, H, W)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((co, ci, kh, kw), dtype=torch.float32, device=dz.device)
+            tdy, tdx = _taps(kh, kw, pad[0], pad[1])
+            wgrad(xp, dzp, tdy, tdx, stride=stride, dw=dw, strides=(ci * kh * kw, kh * kw, 1), co_out=co,
+                  ci_out=ci)
+            dw = dw.to(weight.dtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = channel_sum(dz)
+        return dx, dw, db, None, None, None, None
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
+           pad=0, act: int = ACT_NONE, slope: float = 0.01) -> torch.Tensor:
+    """act(F.conv2d(x, weight, bias, stride, padding)) on NHWC; pad = int or (top, left, bottom, right)
+    (asymmetric: nn.ZeroPad2d((l, r, t, b)) followed by a padding-0 conv)."""
+    if isinstance(pad, int):
+        pad = (pad, pad, pad, pad)
+    return _Conv2dFn.apply(x, weight, bias, int(stride), tuple(pad), int(act), float(slope))
+
+
+# --------------------------------------------------------------------------- ConvTranspose2d
+class _ConvT2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, output_padding, prepad, act, slope):
+        ci, co, kh, kw = weight.shape
+        if x.shape[-1] != ci:
+            raise ValueError(f"conv_transpose2d: input has {x.shape[-1]} channels, weight expects {ci}")
+        xp = _pad_channels(x)
+        B, H, W, _ = x.shape
+        Ho, Wo = Fn.convT_out_hw(H, W, stride, padding, output_padding, kh, prepad)
+        packs = Fn.pack_conv_transpose2d(weight, bias, stride, padding, output_padding, x.dtype, prepad)
+        if xp.shape[-1] != ci:  # padded input channels carry zero weights
+            packs = [ConvPack(w=torch.nn.functional.pad(p.w, (0, Fn._cpad_for(xp.shape[-1], x.dtype) - p.cpad)),
+                              bias=p.bias, ci=xp.shape[-1], co=p.co, dy=p.dy, dx=p.dx, kh=p.kh, kw=p.kw,
+                              stride=p.stride, phase=p.phase) for p in packs]
+        z = Fn.conv_transpose(Act(xp), packs, Ho, Wo).t
+        y = _act_fwd(z, act, slope) if act != ACT_NONE else z
+        ctx.save_for_backward(xp, weight, z if act != ACT_NONE else None)
+        ctx.geom = (stride, padding, prepad, act, slope, H, W, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xp, weight, z = ctx.saved_tensors
+        s, p, prepad, act, slope, H, W, has_bias = ctx.geom
+        ci, co, kh, kw = weight.shape
+        dz = _act_bwd(z, dy, act, slope) if act != ACT_NONE else dy.contiguous()
+        dzp = _pad_channels(dz)
+        # adjoint = conv2d(dz, weight, stride s, padding p) on the pre-padded grid; the
+        # prepad rows/cols are cropped by starting the tap window s*prepad later
+        pt, pl = p - s * prepad[0], p - s * prepad[1]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            pk = Fn.pack_conv2d(weight, None, s, (pt, pl, p, p), dz.dtype, cin_to=dzp.shape[-1])
+            dx = Fn.conv(Act(dzp), pk, out_hw=(H, W)).t
+        if ctx.needs_input_grad[1]:
+            # dW[c, n, ky, kx] = sum_i x[i, c] * dz[s*i + ky - pt, n]: a conv2d weight gradient with
+            # the roles of input (dz) and output gradient (x) exchanged
+            dw = torch.empty((ci, co, kh, kw), dtype=torch.float32, device=dz.device)
+            tdy, tdx = _taps(kh, kw, pt, pl)
+            wgrad(dzp, xp, tdy, tdx, stride=s, lattice=(H, W), dw=dw, strides=(co * kh * kw, kh * kw, 1),
+                  co_out=ci, ci_out=co)
+            dw = dw.to(weight.dtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = channel_sum(dz)
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def conv_transpose2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
+                     padding: int = 0, output_padding: int = 0, prepad: Tuple[int, int] = (0, 0),
+                     act: int = ACT_NONE, slope: float = 0.01) -> torch.Tensor:
+    """act(ConvTranspose2d(ZeroPad2d(left=prepad[1], top=prepad[0])(x))) on NHWC (net_ga.py:373-397)."""
+    return _ConvT2dFn.apply(x, weight, bias, int(stride), int(padding), int(output_padding), tuple(prepad),
+                            int(act), float(slope))
+
+
+# --------------------------------------------------------------------------- GDN / IGDN
+class _GDNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, beta, gamma, bounds, inverse, rsqrt):
+        bb, gb, ped = bounds
+        C = x.shape[-1]
+        if C % _epc(x.dtype):
+            raise ValueError("gdn: channel count must be a multiple of 16 bytes")
+        x = x.contiguous()
+        pk = Fn.gdn_prepare(beta, gamma, bb, gb, ped, x.dtype)
+        nrm = Fn.conv(Act(x), pk, prologue=PRO_SQUARE).t           # beta' + gamma' x^2
+        mode = EPI_GDN_SQRT if inverse else (EPI_GDN_RSQRT if rsqrt else EPI_GDN_DIV)
+        y = Fn.gdn(Act(x), pk, mode).t
+        ctx.save_for_backward(x, nrm, beta, gamma)
+        ctx.cfg = (bb, gb, ped, inverse)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, nrm, beta, gamma = ctx.saved_tensors
+        bb, gb, ped, inverse = ctx.cfg
+        C = x.shape[-1]
+        npix = x.numel() // C
+        dy = dy.contiguous()
+        dxd = torch.empty_like(x)
+        u = torch.empty_like(x)
+        dt = dtype_id(x.dtype)
+        check(_lib().lic_gdn_bwd_elem(dt, _dp(x), C, _dp(nrm), C, _dp(dy), C, npix, C, 1 if inverse else 0,
+                                      _dp(dxd), C, _dp(u), C, stream_handle()))
+        dx = dbeta = dgamma = None
+        if ctx.needs_input_grad[0]:
+            pkt = Fn.gdn_prepare(beta, gamma.detach().t().contiguous(), bb, gb, ped, x.dtype)
+            pkt = ConvPack(w=pkt.w, bias=None, ci=C, co=C, dy=[0], dx=[0])
+            t = Fn.conv(Act(u), pkt).t                                  # gamma'^T u
+            dx = torch.empty_like(x)
+            check(_lib().lic_gdn_bwd_finish(dt, _dp(x), C, _dp(t), C, _dp(dxd), C, npix, C, _dp(dx), C, 0,
+                                            stream_handle()))
+        if ctx.needs_input_grad[1]:
+            dbe = channel_sum(u)
+            dbeta = torch.empty_like(beta, dtype=torch.float32)
+            check(_lib().lic_lower_bound_sq_bwd(_dp(beta.detach().float().contiguous()), _dp(dbe), C, bb,
+                                                _dp(dbeta), 0, stream_handle()))
+        if ctx.needs_input_grad[2]:
+            dge = torch.empty((C, C), dtype=torch.float32, device=x.device)
+            wgrad(x, u, [0], [0], dw=dge, strides=(C, 1, 0), co_out=C, ci_out=C, prologue=PRO_SQUARE)
+            dgamma = torch.empty((C, C), dtype=torch.float32, device=x.device)
+            check(_lib().lic_lower_bound_sq_bwd(_dp(gamma.detach().float().contiguous()), _dp(dge), C * C, gb,
+                                                _dp(dgamma), 0, stream_handle()))
+        return dx, dbeta, dgamma, None, None, None
+
+
+def gdn(x: torch.Tensor, beta: torch.Tensor, gamma: torch.Tensor, beta_bound: float, gamma_bound: float,
+        pedestal: float, inverse: bool = False, rsqrt: bool = False) -> torch.Tensor:
+    """GDN (x / sqrt(n); rsqrt=True: compressai's x * rsqrt(n)) or IGDN (x * sqrt(n)) with
+    n = max(beta,bb)^2-ped + (max(gamma,gb)^2-ped) x^2, on NHWC; gradients through LowerBound."""
+    return _GDNFn.apply(x, beta, gamma, (float(beta_bound), float(gamma_bound), float(pedestal)), bool(inverse),
+                        bool(rsqrt))
+
+
+# --------------------------------------------------------------------------- activations
+class _ActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act, slope):
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        ctx.cfg = (act, slope)
+        return _act_fwd(x, act, slope)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        act, slope = ctx.cfg
+        return _act_bwd(x, dy, act, slope), None, None
+
+
+def activation(x: torch.Tensor, act: int, slope: float = 0.01) -> torch.Tensor:
+    return _ActFn.apply(x, int(act), float(slope))

@@ -10,7 +10,7 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 def _declared():
     txt = (ROOT / "include" / "lic.h").read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(lic_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|const char\*)\s+(lic_\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_header_declares_expected_entry_points():
