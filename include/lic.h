@@ -385,6 +385,82 @@ int lic_gdn_bwd_finish(int32_t dtype, const void* x, int32_t ldx, const void* t,
 int lic_lower_bound_sq_bwd(const float* q, const float* dq_eff, int32_t count, float bound, float* dq,
                            int32_t accumulate, lic_stream_t stream);
 
+/* Window-attention core backward (WBA layers/win_attention.py:85-116, WMSA
+ * model/Block_unet.py:216-252): given the forward args `a` (qkv view, table, mask)
+ * and dO (C channels per pixel), writes dqkv (3C channels: dq | dk | dv) and, if
+ * dtable != NULL, the relative-position-bias gradient (same layout as a.table,
+ * workspace lic_win_attn_bwd_workspace bytes).  Scores and softmax are recomputed
+ * in the forward's op order; window <= 8x8, LDS-resident per (image, window, head). */
+int64_t lic_win_attn_bwd_workspace(const lic_attn_args* a);
+int lic_win_attn_bwd(const lic_attn_args* a, const void* dout, int32_t lddo, void* dqkv, int32_t lddq,
+                     float* dtable, int32_t accumulate_table, float* ws, int64_t ws_bytes,
+                     lic_stream_t stream);
+
+/* nn.LayerNorm(C) backward (net_ga.py:115-127): dx, and dwb = [dweight(C) | dbias(C)]
+ * fp32 (+)=; workspace lic_layernorm_bwd_workspace(npix, c) bytes; C <= 768.          */
+int64_t lic_layernorm_bwd_workspace(int32_t npix, int32_t c);
+int lic_layernorm_bwd(int32_t dtype, const void* x, int32_t ldx, const void* dy, int32_t lddy,
+                      int32_t npix, int32_t c, const float* weight, float eps, void* dx, int32_t lddx,
+                      float* dwb, int32_t accumulate, float* ws, int64_t ws_bytes, lic_stream_t stream);
+
+/* Gate forward y = g * sigmoid(a) (+ r) (r may be NULL), the unfused form the training
+ * path keeps `a` for (layers/layers.py:105-111, net_ga.py:153-174).               */
+int lic_gate_fwd(int32_t dtype, const void* a, int32_t lda, const void* g, int32_t ldg, const void* r,
+                 int32_t ldr, int32_t npix, int32_t c, void* y, int32_t ldy, lic_stream_t stream);
+
+/* LRP refinement y = r + 0.5 tanh(x) (net_ga.py:1060-1062) and its backward
+ * dx = dy * 0.5 (1 - tanh(x)^2) (dr = dy needs no kernel).                        */
+int lic_half_tanh_fwd(int32_t dtype, const void* x, int32_t ldx, const void* r, int32_t ldr, int32_t npix,
+                      int32_t c, void* y, int32_t ldy, lic_stream_t stream);
+int lic_half_tanh_bwd(int32_t dtype, const void* x, int32_t ldx, const void* dy, int32_t lddy,
+                      int32_t npix, int32_t c, void* dx, int32_t lddx, lic_stream_t stream);
+
+/* nn.AdaptiveAvgPool2d(1) backward (Syntax_Model pooling, net_ga.py:627-646):
+ * dx[b, p, c] = dy[b, c] / hw.                                                    */
+int lic_avgpool_bwd(int32_t dtype, const void* dy, int32_t lddy, int32_t n, int32_t hw, int32_t c,
+                    void* dx, int32_t lddx, lic_stream_t stream);
+
+/* Training-mode GaussianConditional (compressai, net_ga.py:1049, mode 'train'):
+ * y~ = y + U(-1/2,1/2) (counter-based noise from `seed` and the element index, so the
+ * backward regenerates it), L' = LowerBound(Phi((1/2-|y~-mu|)/s) - Phi((-1/2-|y~-mu|)/s),
+ * 1e-9), s = LowerBound(scale, 0.11); partials[block] = sum ln L' (fp64,
+ * lic_rate_train_parts blocks); yhat (may be NULL) = rint(y-mu)+mu (ste_round forward).
+ * bwd: with gout = dLoss/dbpp (device fp32 scalar) and factor = -1/(ln2 * num_pixels):
+ * dy, dmu, dscale of factor * gout * sum ln L' (LowerBound gradient rules).       */
+int32_t lic_rate_train_parts(int32_t npix, int32_t c);
+int lic_rate_train_fwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
+                       const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                       float scale_bound, float likelihood_bound, void* yhat, int32_t ldyh,
+                       double* partials, lic_stream_t stream);
+int lic_rate_train_bwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
+                       const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                       float scale_bound, float likelihood_bound, const float* gout, float factor,
+                       void* dy, int32_t lddy, void* dmu, int32_t lddmu, void* dscale, int32_t lddsc,
+                       lic_stream_t stream);
+
+/* Training reconstruction head: x~ = tanh(W_b x16) per image (batch_conv + tanh,
+ * net_ga.py:969-979,1092), xt (NCHW fp32, may be NULL), per-(image, block) squared
+ * error partials vs img (NCHW fp32) for nn.MSELoss (net_ga.py:1115).  bwd with
+ * gout = dLoss/dmse (device scalar), factor = 2/(B*3*H*W): dx16 and dW_b (fp32
+ * [n][3*cin]); workspace n * lic_recon_train_blocks(hw) * 3 * cin floats.          */
+int32_t lic_recon_train_blocks(int32_t hw);
+int lic_recon_train_fwd(int32_t dtype, const void* x16, int32_t ldx, int32_t n, int32_t hw, int32_t cin,
+                        const void* wgen, int32_t ldw, const float* img, float* xt, double* partials,
+                        lic_stream_t stream);
+int lic_recon_train_bwd(int32_t dtype, const void* x16, int32_t ldx, int32_t n, int32_t hw, int32_t cin,
+                        const void* wgen, int32_t ldw, const float* img, const float* gout, float factor,
+                        void* dx16, int32_t lddx, float* dw, float* ws, int64_t ws_bytes,
+                        lic_stream_t stream);
+
+/* Depthwise (groups = C) conv weight gradient, dw fp32 in torch [C, 1, kh, kw] order
+ * (Syntax_Model's DepthwiseSeparableConv, net_ga.py:613-619).  Tap offsets are host
+ * arrays (copied into the kernel arguments).                                       */
+int64_t lic_dwconv_wgrad_workspace(int32_t n, int32_t ho, int32_t wo, int32_t c, int32_t ntaps);
+int lic_dwconv_wgrad(int32_t dtype, const void* x, int32_t ldx, const void* dz, int32_t ldz, int32_t n,
+                     int32_t h, int32_t w, int32_t ho, int32_t wo, int32_t c, int32_t stride,
+                     int32_t ntaps, const int8_t* dy, const int8_t* dx, float* dw, float* ws,
+                     int64_t ws_bytes, lic_stream_t stream);
+
 /* Library info. */
 const char* lic_last_error(void);
 const char* lic_version(void);

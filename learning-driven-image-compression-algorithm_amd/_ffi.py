@@ -29,7 +29,10 @@ EXPORTED_SYMBOLS = (
     "lic_pool_partials", "lic_ca_apply_fwd", "lic_lam_parts", "lic_lam_fwd", "lic_csam_fwd", "lic_recon_fwd",
     "lic_conv2d_wgrad_workspace", "lic_conv2d_wgrad", "lic_channel_sum_workspace", "lic_channel_sum",
     "lic_act_fwd", "lic_act_bwd", "lic_gate_bwd", "lic_gdn_bwd_elem", "lic_gdn_bwd_finish",
-    "lic_lower_bound_sq_bwd",
+    "lic_lower_bound_sq_bwd", "lic_win_attn_bwd_workspace", "lic_win_attn_bwd", "lic_layernorm_bwd_workspace",
+    "lic_layernorm_bwd", "lic_gate_fwd", "lic_half_tanh_fwd", "lic_half_tanh_bwd", "lic_avgpool_bwd",
+    "lic_rate_train_parts", "lic_rate_train_fwd", "lic_rate_train_bwd", "lic_recon_train_blocks",
+    "lic_recon_train_fwd", "lic_recon_train_bwd", "lic_dwconv_wgrad_workspace", "lic_dwconv_wgrad",
 )
 LIC_EB_PARAMS = 58
 
@@ -146,6 +149,7 @@ def load():
                        "or __graft_entry__.build().")
         raise LicError(_load_error) from e
     I, V, F, D, L = ctypes.c_int32, ctypes.c_void_p, ctypes.c_float, ctypes.c_double, ctypes.c_int64
+    U = ctypes.c_uint64
     sig = {
         "lic_conv2d_fwd": [V, V],
         "lic_gdn_prepare": [I, V, V, I, F, F, F, V, I, I, V, V],
@@ -184,6 +188,17 @@ def load():
         "lic_gdn_bwd_elem": [I, V, I, V, I, V, I, I, I, I, V, I, V, I, V],
         "lic_gdn_bwd_finish": [I, V, I, V, I, V, I, I, I, V, I, I, V],
         "lic_lower_bound_sq_bwd": [V, V, I, F, V, I, V],
+        "lic_win_attn_bwd": [V, V, I, V, I, V, I, V, L, V],
+        "lic_layernorm_bwd": [I, V, I, V, I, I, I, V, F, V, I, V, I, V, L, V],
+        "lic_gate_fwd": [I, V, I, V, I, V, I, I, I, V, I, V],
+        "lic_half_tanh_fwd": [I, V, I, V, I, I, I, V, I, V],
+        "lic_half_tanh_bwd": [I, V, I, V, I, I, I, V, I, V],
+        "lic_avgpool_bwd": [I, V, I, I, I, I, V, I, V],
+        "lic_rate_train_fwd": [I, V, I, V, I, V, I, I, I, U, F, F, V, I, V, V],
+        "lic_rate_train_bwd": [I, V, I, V, I, V, I, I, I, U, F, F, V, F, V, I, V, I, V, I, V],
+        "lic_recon_train_fwd": [I, V, I, I, I, I, V, I, V, V, V, V],
+        "lic_recon_train_bwd": [I, V, I, I, I, I, V, I, V, V, F, V, I, V, V, L, V],
+        "lic_dwconv_wgrad": [I, V, I, V, I, I, I, I, I, I, I, I, I, V, V, V, V, L, V],
     }
     for name, argt in sig.items():
         fn = getattr(lib, name)
@@ -197,6 +212,13 @@ def load():
     lib.lic_conv2d_wgrad_workspace.restype = ctypes.c_int64
     lib.lic_channel_sum_workspace.argtypes = [I]
     lib.lic_channel_sum_workspace.restype = ctypes.c_int64
+    for name, argt in (("lic_win_attn_bwd_workspace", [V]), ("lic_layernorm_bwd_workspace", [I, I]),
+                       ("lic_dwconv_wgrad_workspace", [I, I, I, I, I])):
+        getattr(lib, name).argtypes = argt
+        getattr(lib, name).restype = ctypes.c_int64
+    for name, argt in (("lic_rate_train_parts", [I, I]), ("lic_recon_train_blocks", [I])):
+        getattr(lib, name).argtypes = argt
+        getattr(lib, name).restype = ctypes.c_int32
     lib.lic_last_error.restype = ctypes.c_char_p
     lib.lic_version.restype = ctypes.c_char_p
     _lib = lib

@@ -21,13 +21,14 @@ gradients come back fp32 in those layouts.  There is no PyTorch compute fallback
 from __future__ import annotations
 
 import ctypes
+import math
 from typing import Optional, Sequence, Tuple
 
 import torch
 
 from . import _ffi
 from . import functional as Fn
-from ._ffi import ACT_NONE, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, PRO_NONE, PRO_SQUARE, WgradArgs, check
+from ._ffi import ACT_NONE, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, PRO_NONE, PRO_SQUARE, AttnArgs, WgradArgs, check
 from .functional import Act, ConvPack, _dp, dtype_id, stream_handle
 
 __all__ = ["conv2d", "conv_transpose2d", "gdn", "activation", "wgrad", "channel_sum", "dgrad_packs"]
@@ -348,3 +349,338 @@ class _ActFn(torch.autograd.Function):
 
 def activation(x: torch.Tensor, act: int, slope: float = 0.01) -> torch.Tensor:
     return _ActFn.apply(x, int(act), float(slope))
+
+
+# --------------------------------------------------------------------------- layout / elementwise
+def to_nhwc(x_nchw: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """Input image NCHW fp32 -> NHWC activation tensor (lic_nchw_to_nhwc); the image is a leaf."""
+    return Act.from_nchw(x_nchw.detach().contiguous(), dtype).t
+
+
+def _npix(t: torch.Tensor) -> int:
+    return t.numel() // t.shape[-1]
+
+
+def _add_raw(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    a, b = a.contiguous(), b.contiguous()
+    C = a.shape[-1]
+    out = torch.empty_like(a)
+    check(_lib().lic_add(dtype_id(a.dtype), _dp(a), C, _dp(b), C, _npix(a), C, _dp(out), C, stream_handle()))
+    return out
+
+
+class _AddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        return _add_raw(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a + b (the residual adds)."""
+    return _AddFn.apply(a, b)
+
+
+class _GateFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, b, a, r):
+        b, a, r = b.contiguous(), a.contiguous(), r.contiguous()
+        C = a.shape[-1]
+        y = torch.empty_like(a)
+        check(_lib().lic_gate_fwd(dtype_id(a.dtype), _dp(b), C, _dp(a), C, _dp(r), C, _npix(a), C, _dp(y), C,
+                                  stream_handle()))
+        ctx.save_for_backward(b, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        b, a = ctx.saved_tensors
+        g = g.contiguous()
+        C = a.shape[-1]
+        db, da = torch.empty_like(b), torch.empty_like(a)
+        check(_lib().lic_gate_bwd(dtype_id(a.dtype), _dp(b), C, _dp(a), C, _dp(g), C, _npix(a), C, _dp(db), C,
+                                  _dp(da), C, stream_handle()))
+        return db, da, g
+
+
+def gate(b: torch.Tensor, a: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """a * sigmoid(b) + r (Win_noShift_Attention / AttentionBlock gate, layers/layers.py:105-111)."""
+    return _GateFn.apply(b, a, r)
+
+
+class _HalfTanhFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r):
+        x, r = x.contiguous(), r.contiguous()
+        C = x.shape[-1]
+        y = torch.empty_like(r)
+        check(_lib().lic_half_tanh_fwd(dtype_id(x.dtype), _dp(x), C, _dp(r), C, _npix(x), C, _dp(y), C,
+                                       stream_handle()))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        g = g.contiguous()
+        C = x.shape[-1]
+        dx = torch.empty_like(x)
+        check(_lib().lic_half_tanh_bwd(dtype_id(x.dtype), _dp(x), C, _dp(g), C, _npix(x), C, _dp(dx), C,
+                                       stream_handle()))
+        return dx, g
+
+
+def half_tanh_add(x: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """r + 0.5 * tanh(x) (LRP refinement, net_ga.py:1060-1062)."""
+    return _HalfTanhFn.apply(x, r)
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        B, H, W, C = x.shape
+        out = torch.empty((B, 1, 1, C), dtype=x.dtype, device=x.device)
+        Fn.avgpool(Act(x), Act(out))
+        ctx.shape = (B, H, W, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, H, W, C = ctx.shape
+        g = g.contiguous()
+        dx = torch.empty((B, H, W, C), dtype=g.dtype, device=g.device)
+        check(_lib().lic_avgpool_bwd(dtype_id(g.dtype), _dp(g), C, B, H * W, C, _dp(dx), C, stream_handle()))
+        return dx
+
+
+def avgpool(x: torch.Tensor) -> torch.Tensor:
+    """nn.AdaptiveAvgPool2d(1) on NHWC -> [B, 1, 1, C]."""
+    return _AvgPoolFn.apply(x)
+
+
+class _SteQuantFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, medians):
+        return Fn.quantize_median(Act(z.contiguous()), medians).t
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+def ste_quantize(z: torch.Tensor, medians: Optional[torch.Tensor]) -> torch.Tensor:
+    """ste_round(z - m) + m (net_ga.py:996-1003): rounded forward, identity gradient."""
+    return _SteQuantFn.apply(z, medians)
+
+
+# --------------------------------------------------------------------------- LayerNorm / attention
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        x = x.contiguous()
+        w = weight.detach().float().contiguous()
+        y = Fn.layernorm(Act(x), w, bias.detach().float().contiguous(), eps).t
+        ctx.save_for_backward(x, w)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g = g.contiguous()
+        C = x.shape[-1]
+        npix = _npix(x)
+        dx = torch.empty_like(x)
+        dwb = torch.empty((2 * C,), dtype=torch.float32, device=x.device)
+        nbytes = int(_lib().lic_layernorm_bwd_workspace(npix, C))
+        ws = torch.empty((nbytes // 4 + 1,), dtype=torch.float32, device=x.device)
+        check(_lib().lic_layernorm_bwd(dtype_id(x.dtype), _dp(x), C, _dp(g), C, npix, C, _dp(w), ctx.eps, _dp(dx),
+                                       C, _dp(dwb), 0, _dp(ws), nbytes, stream_handle()))
+        return dx, dwb[:C], dwb[C:], None
+
+
+def layernorm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float) -> torch.Tensor:
+    """nn.LayerNorm(C) over the channels of every pixel (net_ga.py:115-127)."""
+    return _LayerNormFn.apply(x, weight, bias, float(eps))
+
+
+def _attn_args(qkv, table, C, heads, ws, shift, tab_sr, tab_sh, mask_kind, scale_after, scale):
+    B, H, W, _ = qkv.shape
+    a = AttnArgs()
+    a.dtype = dtype_id(qkv.dtype)
+    a.qkv, a.n, a.h, a.w, a.c, a.ldqkv = _dp(qkv), B, H, W, C, qkv.shape[-1]
+    a.out, a.ldo = None, C
+    a.heads, a.ws, a.shift = heads, ws, shift
+    a.table, a.tab_sr, a.tab_sh = _dp(table), tab_sr, tab_sh
+    a.mask_kind, a.scale_after, a.scale = mask_kind, 1 if scale_after else 0, scale
+    a.force_valu = 0
+    return a
+
+
+class _WinAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, table, cfg):
+        C, heads, ws, shift, tab_sr, tab_sh, mask_kind, scale_after, scale = cfg
+        qkv = qkv.contiguous()
+        tab = table.detach().float().contiguous()
+        out = Fn.win_attn(Act(qkv), C, heads, ws, shift, tab, tab_sr, tab_sh, mask_kind, scale_after, scale).t
+        ctx.save_for_backward(qkv, tab)
+        ctx.cfg = cfg
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        qkv, tab = ctx.saved_tensors
+        C = ctx.cfg[0]
+        g = g.contiguous()
+        a = _attn_args(qkv, tab, *ctx.cfg)
+        dqkv = torch.empty_like(qkv)
+        dtab = torch.empty_like(tab) if ctx.needs_input_grad[1] else None
+        need = int(_lib().lic_win_attn_bwd_workspace(ctypes.byref(a)))
+        ws = torch.empty((max(need, 4) // 4,), dtype=torch.float32, device=qkv.device)
+        check(_lib().lic_win_attn_bwd(ctypes.byref(a), _dp(g), C, _dp(dqkv), qkv.shape[-1],
+                                      _dp(dtab) if dtab is not None else None, 0, _dp(ws), need, stream_handle()))
+        return dqkv, dtab, None
+
+
+def win_attn(qkv: torch.Tensor, table: torch.Tensor, C: int, heads: int, ws: int, shift: int, *, tab_sr: int,
+             tab_sh: int, mask_kind: int, scale_after: bool, scale: float) -> torch.Tensor:
+    """Window-attention core over a [B, H, W, 3C] qkv tensor (lic_win_attn_fwd / lic_win_attn_bwd):
+    WBA (layers/win_attention.py:85-116) or WMSA (model/Block_unet.py:216-252)."""
+    return _WinAttnFn.apply(qkv, table, (int(C), int(heads), int(ws), int(shift), int(tab_sr), int(tab_sh),
+                                         int(mask_kind), bool(scale_after), float(scale)))
+
+
+# --------------------------------------------------------------------------- rate / reconstruction
+class _RateTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, mu, sc, cfg):
+        seed, num_pixels, sb, lb = cfg
+        y, mu, sc = y.contiguous(), mu.contiguous(), sc.contiguous()
+        C = y.shape[-1]
+        npix = _npix(y)
+        nparts = int(_lib().lic_rate_train_parts(npix, C))
+        parts = torch.empty((max(nparts, 1),), dtype=torch.float64, device=y.device)
+        yhat = torch.empty_like(y)
+        check(_lib().lic_rate_train_fwd(dtype_id(y.dtype), _dp(y), C, _dp(mu), C, _dp(sc), C, npix, C, seed, sb, lb,
+                                        _dp(yhat), C, _dp(parts), stream_handle()))
+        bpp = torch.empty((), dtype=torch.float32, device=y.device)
+        Fn.bpp_finalize(parts, nparts, num_pixels, bpp)
+        ctx.save_for_backward(y, mu, sc)
+        ctx.cfg = cfg
+        return bpp, yhat
+
+    @staticmethod
+    def backward(ctx, gb, gy):
+        y, mu, sc = ctx.saved_tensors
+        seed, num_pixels, sb, lb = ctx.cfg
+        C = y.shape[-1]
+        npix = _npix(y)
+        if gb is None:
+            gb = torch.zeros((), dtype=torch.float32, device=y.device)
+        gout = gb.detach().float().reshape(1).contiguous()
+        dy, dmu, dsc = torch.empty_like(y), torch.empty_like(mu), torch.empty_like(sc)
+        check(_lib().lic_rate_train_bwd(dtype_id(y.dtype), _dp(y), C, _dp(mu), C, _dp(sc), C, npix, C, seed, sb, lb,
+                                        _dp(gout), -1.0 / (math.log(2.0) * num_pixels), _dp(dy), C, _dp(dmu), C,
+                                        _dp(dsc), C, stream_handle()))
+        if gy is not None:   # ste_round(y - mu) + mu: d/dy = 1, d/dmu = 0
+            dy = _add_raw(dy, gy)
+        return dy, dmu, dsc, None
+
+
+def rate_train(y: torch.Tensor, mu: torch.Tensor, scale: torch.Tensor, seed: int, num_pixels: float,
+               scale_bound: float = 0.11, likelihood_bound: float = 1e-9):
+    """Training-mode GaussianConditional of one slice (net_ga.py:1049 with noise) -> (bpp contribution
+    sum ln L / (-ln 2 * num_pixels) as a 0-d fp32 tensor, ste_round(y - mu) + mu)."""
+    return _RateTrainFn.apply(y, mu, scale, (int(seed) & (2 ** 64 - 1), float(num_pixels), float(scale_bound),
+                                             float(likelihood_bound)))
+
+
+class _ReconMSEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x16, cw, img):
+        x16, cw, img = x16.contiguous(), cw.contiguous(), img.contiguous()
+        B, H, W, C = x16.shape
+        nblk = int(_lib().lic_recon_train_blocks(H * W))
+        parts = torch.empty((B * nblk,), dtype=torch.float64, device=x16.device)
+        check(_lib().lic_recon_train_fwd(dtype_id(x16.dtype), _dp(x16), C, B, H * W, C, _dp(cw), cw.shape[-1],
+                                         _dp(img), None, _dp(parts), stream_handle()))
+        n = B * 3 * H * W
+        mse = torch.empty((), dtype=torch.float32, device=x16.device)
+        Fn.bpp_finalize(parts, B * nblk, -n / math.log(2.0), mse)     # = sum / n
+        ctx.save_for_backward(x16, cw, img)
+        return mse
+
+    @staticmethod
+    def backward(ctx, g):
+        x16, cw, img = ctx.saved_tensors
+        B, H, W, C = x16.shape
+        nblk = int(_lib().lic_recon_train_blocks(H * W))
+        gout = g.detach().float().reshape(1).contiguous()
+        dx16 = torch.empty_like(x16)
+        dw = torch.empty((B, 3 * C), dtype=torch.float32, device=x16.device)
+        ws = torch.empty((B * nblk * 3 * C,), dtype=torch.float32, device=x16.device)
+        check(_lib().lic_recon_train_bwd(dtype_id(x16.dtype), _dp(x16), C, B, H * W, C, _dp(cw), cw.shape[-1],
+                                         _dp(img), _dp(gout), 2.0 / (B * 3 * H * W), _dp(dx16), C, _dp(dw), _dp(ws),
+                                         ws.numel() * 4, stream_handle()))
+        return dx16, dw.view(B, 1, 1, 3 * C).to(cw.dtype), None
+
+
+def recon_mse(x16: torch.Tensor, cw: torch.Tensor, img: torch.Tensor) -> torch.Tensor:
+    """nn.MSELoss()(tanh(batch_conv(cw, x16)), img) (net_ga.py:1089-1092, :1115); x16 NHWC, cw
+    [B, 1, 1, 3*C] (row-major (3, C)), img NCHW fp32."""
+    return _ReconMSEFn.apply(x16, cw, img)
+
+
+# --------------------------------------------------------------------------- depthwise conv
+class _DwConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad):
+        x = x.contiguous()
+        C = x.shape[-1]
+        pk = Fn.pack_conv2d(weight, bias, stride, pad, x.dtype, groups=C)
+        z = Fn.conv(Act(x), pk).t
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (stride, pad, bias is not None, z.shape[1], z.shape[2])
+        return z
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        stride, pad, has_bias, Ho, Wo = ctx.cfg
+        B, H, W, C = x.shape
+        kh, kw = weight.shape[2], weight.shape[3]
+        g = g.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if stride != 1:
+                raise NotImplementedError("depthwise conv backward: stride 1 only (Syntax_Model)")
+            pt, pl, pb, pr = pad
+            pk = Fn.pack_conv2d(weight.detach().flip(2, 3), None, 1,
+                                (kh - 1 - pt, kw - 1 - pl, kh - 1 - pb, kw - 1 - pr), g.dtype, groups=C)
+            dx = Fn.conv(Act(g), pk, out_hw=(H, W)).t
+        if ctx.needs_input_grad[1]:
+            tdy, tdx = _taps(kh, kw, pad[0], pad[1])
+            n = len(tdy)
+            ady, adx = (ctypes.c_int8 * n)(*tdy), (ctypes.c_int8 * n)(*tdx)
+            need = int(_lib().lic_dwconv_wgrad_workspace(B, Ho, Wo, C, n))
+            ws = torch.empty((max(need, 4) // 4,), dtype=torch.float32, device=x.device)
+            dw = torch.empty((C, 1, kh, kw), dtype=torch.float32, device=x.device)
+            check(_lib().lic_dwconv_wgrad(dtype_id(x.dtype), _dp(x), C, _dp(g), C, B, H, W, Ho, Wo, C, stride, n,
+                                          ctypes.cast(ady, ctypes.c_void_p), ctypes.cast(adx, ctypes.c_void_p),
+                                          _dp(dw), _dp(ws), need, stream_handle()))
+            dw = dw.to(weight.dtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = channel_sum(g)
+        return dx, dw, db, None, None
+
+
+def dwconv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad) -> torch.Tensor:
+    """Depthwise nn.Conv2d (groups = C) on NHWC (DepthwiseSeparableConv, UNPINNED restatement)."""
+    if isinstance(pad, int):
+        pad = (pad,) * 4
+    return _DwConvFn.apply(x, weight, bias, int(stride), tuple(pad))

@@ -378,6 +378,485 @@ __global__ void lower_bound_sq_bwd_kernel(const float* __restrict__ q, const flo
   dq[i] = accumulate ? dq[i] + r : r;
 }
 
+
+__device__ __forceinline__ double block_sum_f64_256(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+struct DwTaps { int8_t dy[LIC_MAX_TAPS]; int8_t dx[LIC_MAX_TAPS]; };
+
+// ---------------------------------------------------------------------------- window attention bwd
+// One 256-thread work-group per (image, window, head).  q, k, v, dO of the window are
+// staged in LDS as fp32 (same roll / partition address arithmetic as the forward),
+// the scores are recomputed in the forward's op order, then
+//   D_i = sum_j P_ij (dO_i . v_j);  dV_j = sum_i P_ij dO_i;  dS_ij = P_ij (dO_i . v_j - D_i)
+//   dQ_i = scale sum_j dS_ij k_j;   dK_j = scale sum_i dS_ij q_i
+// and the relative-position-bias gradient is accumulated per work-group in LDS
+// (one partial per (head, window, offset); deterministic second-pass reduce).
+template <typename T>
+__global__ __launch_bounds__(256) void win_attn_bwd_kernel(const lic_attn_args a, const T* __restrict__ dout,
+                                                           int lddo, T* __restrict__ dqkv, int lddq,
+                                                           float* __restrict__ tparts) {
+  const int ws = a.ws, N = ws * ws, d = a.c / a.heads, dp = d + 1;
+  const int R = (2 * ws - 1) * (2 * ws - 1);
+  const int nwx = a.w / ws, nwy = a.h / ws;
+  int bid = blockIdx.x;
+  const int h = bid % a.heads;
+  bid /= a.heads;
+  const int win = bid;  // (b * nwy + wy) * nwx + wx
+  const int wx = bid % nwx;
+  bid /= nwx;
+  const int wy = bid % nwy;
+  const int b = bid / nwy;
+  const int nwin = a.n * nwy * nwx;
+
+  extern __shared__ float sm[];
+  float* sq = sm;
+  float* sk = sq + N * dp;
+  float* sv = sk + N * dp;
+  float* sdo = sv + N * dp;
+  float* sP = sdo + N * dp;          // [N][N+1]
+  float* sD = sP + N * (N + 1);      // [N]
+  float* stab = sD + N;              // [R]
+  const int tid = threadIdx.x;
+
+  auto pix = [&](int t) -> int64_t {
+    const int sy = wy * ws + t / ws, sx = wx * ws + t % ws;
+    int py = sy + a.shift, px = sx + a.shift;
+    if (py >= a.h) py -= a.h;
+    if (px >= a.w) px -= a.w;
+    return ((int64_t)b * a.h + py) * a.w + px;
+  };
+  const T* qkv = (const T*)a.qkv;
+  for (int e = tid; e < N * d; e += 256) {
+    const int t = e / d, c = e % d;
+    const int64_t p = pix(t);
+    const T* q = qkv + p * a.ldqkv + h * d + c;
+    sq[t * dp + c] = to_f(q[0]);
+    sk[t * dp + c] = to_f(q[a.c]);
+    sv[t * dp + c] = to_f(q[2 * a.c]);
+    sdo[t * dp + c] = to_f(dout[p * lddo + h * d + c]);
+  }
+  for (int r = tid; r < R; r += 256) stab[r] = 0.f;
+  __syncthreads();
+
+  const float scale = a.scale;
+  auto reg_wba = [&](int y, int x) {
+    const int ly = y < a.h - ws ? 0 : (y < a.h - a.shift ? 1 : 2);
+    const int lx = x < a.w - ws ? 0 : (x < a.w - a.shift ? 1 : 2);
+    return ly * 3 + lx;
+  };
+  const int split = ws - a.shift;
+  const bool last_row = (wy == nwy - 1), last_col = (wx == nwx - 1);
+  auto relidx = [&](int i, int j) {
+    return (i / ws - j / ws + ws - 1) * (2 * ws - 1) + (i % ws - j % ws + ws - 1);
+  };
+  for (int e = tid; e < N * N; e += 256) {
+    const int i = e / N, j = e % N;
+    float dot = 0.f;
+    for (int c = 0; c < d; ++c) {
+      const float qv = a.scale_after ? sq[i * dp + c] : sq[i * dp + c] * scale;
+      dot += qv * sk[j * dp + c];
+    }
+    if (a.scale_after) dot = dot * scale;
+    float v = dot + a.table[relidx(i, j) * a.tab_sr + h * a.tab_sh];
+    const int iy = i / ws, ix = i % ws, jy = j / ws, jx = j % ws;
+    if (a.mask_kind == 1) {
+      if (reg_wba(wy * ws + jy, wx * ws + jx) != reg_wba(wy * ws + iy, wx * ws + ix)) v += -100.0f;
+    } else if (a.mask_kind == 2) {
+      bool m = false;
+      if (last_row && ((iy < split) != (jy < split))) m = true;
+      if (last_col && ((ix < split) != (jx < split))) m = true;
+      if (m) v = -INFINITY;
+    }
+    sP[i * (N + 1) + j] = v;
+  }
+  __syncthreads();
+  if (tid < N) {
+    float* row = sP + tid * (N + 1);
+    float mx = -INFINITY;
+    for (int j = 0; j < N; ++j) mx = fmaxf(mx, row[j]);
+    float sum = 0.f;
+    for (int j = 0; j < N; ++j) {
+      row[j] = expf(row[j] - mx);
+      sum += row[j];
+    }
+    const float inv = 1.0f / sum;
+    for (int j = 0; j < N; ++j) row[j] *= inv;
+  }
+  __syncthreads();
+  if (tid < N) {
+    const float* row = sP + tid * (N + 1);
+    float acc = 0.f;
+    for (int j = 0; j < N; ++j) {
+      float dpv = 0.f;
+      for (int c = 0; c < d; ++c) dpv += sdo[tid * dp + c] * sv[j * dp + c];
+      acc += row[j] * dpv;
+    }
+    sD[tid] = acc;
+  }
+  for (int e = tid; e < N * d; e += 256) {  // dV
+    const int j = e / d, c = e % d;
+    float acc = 0.f;
+    for (int i = 0; i < N; ++i) acc += sP[i * (N + 1) + j] * sdo[i * dp + c];
+    dqkv[pix(j) * lddq + 2 * a.c + h * d + c] = from_f<T>(acc);
+  }
+  __syncthreads();
+  for (int e = tid; e < N * N; e += 256) {  // dS (in place of P)
+    const int i = e / N, j = e % N;
+    float dpv = 0.f;
+    for (int c = 0; c < d; ++c) dpv += sdo[i * dp + c] * sv[j * dp + c];
+    const float ds = sP[i * (N + 1) + j] * (dpv - sD[i]);
+    sP[i * (N + 1) + j] = ds;
+    atomicAdd(&stab[relidx(i, j)], ds);
+  }
+  __syncthreads();
+  for (int e = tid; e < N * d; e += 256) {
+    const int i = e / d, c = e % d;
+    float aq = 0.f, ak = 0.f;
+    for (int j = 0; j < N; ++j) {
+      aq += sP[i * (N + 1) + j] * sk[j * dp + c];
+      ak += sP[j * (N + 1) + i] * sq[j * dp + c];
+    }
+    const int64_t p = pix(i);
+    dqkv[p * lddq + h * d + c] = from_f<T>(aq * scale);
+    dqkv[p * lddq + a.c + h * d + c] = from_f<T>(ak * scale);
+  }
+  if (tparts)
+    for (int r = tid; r < R; r += 256) tparts[((int64_t)h * nwin + win) * R + r] = stab[r];
+}
+
+__global__ void attn_table_reduce_kernel(const float* __restrict__ parts, int heads, int nwin, int R,
+                                         float* __restrict__ dtab, int tab_sr, int tab_sh, int accumulate) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= heads * R) return;
+  const int h = idx / R, r = idx % R;
+  const float* p = parts + (int64_t)h * nwin * R + r;
+  float s = 0.f;
+  for (int k = 0; k < nwin; ++k) s += p[(int64_t)k * R];
+  float* o = dtab + r * tab_sr + h * tab_sh;
+  *o = accumulate ? *o + s : s;
+}
+
+// ---------------------------------------------------------------------------- LayerNorm bwd
+// One wave per pixel (grid-stride), lane owns channels lane + 64 m.  dx = rstd (g - mean(g)
+// - xhat mean(g xhat)), g = dy * w; dw / db accumulated per lane, then per block.
+template <typename T, int CPL>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ x, int ldx,
+                                                            const T* __restrict__ dy, int lddy, int npix, int c,
+                                                            const float* __restrict__ wt, float eps,
+                                                            T* __restrict__ dx, int lddx, float* __restrict__ parts) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dw[CPL], db[CPL];
+#pragma unroll
+  for (int m = 0; m < CPL; ++m) dw[m] = db[m] = 0.f;
+  for (int64_t p = (int64_t)blockIdx.x * 4 + wave; p < npix; p += (int64_t)gridDim.x * 4) {
+    const T* xp = x + p * ldx;
+    const T* gp = dy + p * lddy;
+    float xv[CPL], gv[CPL];
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < CPL; ++m) {
+      const int k = lane + 64 * m;
+      xv[m] = k < c ? to_f(xp[k]) : 0.f;
+      gv[m] = k < c ? to_f(gp[k]) : 0.f;
+      s += xv[m];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)c;
+    float v = 0.f;
+#pragma unroll
+    for (int m = 0; m < CPL; ++m) {
+      const float dd = lane + 64 * m < c ? xv[m] - mean : 0.f;
+      v += dd * dd;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const float rstd = 1.0f / sqrtf(v / (float)c + eps);
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int m = 0; m < CPL; ++m) {
+      const int k = lane + 64 * m;
+      if (k < c) {
+        const float xh = (xv[m] - mean) * rstd;
+        const float g = gv[m] * wt[k];
+        sg += g;
+        sgx += g * xh;
+        dw[m] += gv[m] * xh;
+        db[m] += gv[m];
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      sg += __shfl_xor(sg, o);
+      sgx += __shfl_xor(sgx, o);
+    }
+    sg /= (float)c;
+    sgx /= (float)c;
+    T* op = dx + p * lddx;
+#pragma unroll
+    for (int m = 0; m < CPL; ++m) {
+      const int k = lane + 64 * m;
+      if (k < c) {
+        const float xh = (xv[m] - mean) * rstd;
+        op[k] = from_f<T>(rstd * (gv[m] * wt[k] - sg - xh * sgx));
+      }
+    }
+  }
+  __shared__ float red[4][2 * 64 * CPL];
+#pragma unroll
+  for (int m = 0; m < CPL; ++m) {
+    red[wave][m * 64 + lane] = dw[m];
+    red[wave][64 * CPL + m * 64 + lane] = db[m];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < c; k += 256) {
+    const int m = k / 64, l = k % 64;
+    float sw = 0.f, sb = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sw += red[q][m * 64 + l];
+      sb += red[q][64 * CPL + m * 64 + l];
+    }
+    parts[(int64_t)blockIdx.x * 2 * c + k] = sw;
+    parts[(int64_t)blockIdx.x * 2 * c + c + k] = sb;
+  }
+}
+
+// ---------------------------------------------------------------------------- gate fwd
+template <typename T>
+__global__ void gate_fwd_kernel(const T* __restrict__ av, int lda, const T* __restrict__ g, int ldg,
+                                const T* __restrict__ r, int ldr, int npix, int c, T* __restrict__ y, int ldy) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)npix * c) return;
+  const int64_t p = idx / c;
+  const int ch = (int)(idx - p * c);
+  float v = to_f(g[p * ldg + ch]) * sigmoid_f(to_f(av[p * lda + ch]));
+  if (r) v += to_f(r[p * ldr + ch]);
+  y[p * ldy + ch] = from_f<T>(v);
+}
+
+// ---------------------------------------------------------------------------- rate (train mode)
+// compressai GaussianConditional.forward(y, scale, mu) with training=True: y~ = y + U(-1/2, 1/2)
+// (counter-based hash noise: (seed, element index) -> uniform), L = Phi((1/2-|y~-mu|)/s) -
+// Phi((-1/2-|y~-mu|)/s), s = LowerBound(scale, 0.11), L' = LowerBound(L, 1e-9); plus the
+// ste_round forward yhat = rint(y - mu) + mu (net_ga.py:1053).
+__device__ __forceinline__ float noise_u(uint64_t seed, uint64_t i) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + i;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f) - 0.5f;  // 24-bit uniform in [-1/2, 1/2)
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rate_train_fwd_kernel(const T* __restrict__ y, int ldy, const T* __restrict__ mu,
+                                                             int ldmu, const T* __restrict__ sc, int ldsc, int npix,
+                                                             int c, uint64_t seed, float sbound, float lbound,
+                                                             T* __restrict__ yhat, int ldyh, double* __restrict__ parts) {
+  __shared__ double red[4];
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double acc = 0.0;
+  if (idx < (int64_t)npix * c) {
+    const int64_t p = idx / c;
+    const int k = (int)(idx - p * c);
+    const float yv = to_f(y[p * ldy + k]);
+    const float m = to_f(mu[p * ldmu + k]);
+    const float v = fabsf((yv + noise_u(seed, (uint64_t)idx)) - m);
+    const float s = fmaxf(to_f(sc[p * ldsc + k]), sbound);
+    const float cst = -0.70710678118654752440f;
+    const float L = 0.5f * erfcf(cst * ((0.5f - v) / s)) - 0.5f * erfcf(cst * ((-0.5f - v) / s));
+    acc = (double)logf(fmaxf(L, lbound));
+    if (yhat) yhat[p * ldyh + k] = from_f<T>(rintf(yv - m) + m);
+  }
+  const double t = block_sum_f64_256(acc, red);
+  if (threadIdx.x == 0) parts[blockIdx.x] = t;
+}
+
+template <typename T>
+__global__ void rate_train_bwd_kernel(const T* __restrict__ y, int ldy, const T* __restrict__ mu, int ldmu,
+                                      const T* __restrict__ sc, int ldsc, int npix, int c, uint64_t seed,
+                                      float sbound, float lbound, const float* __restrict__ gout, float factor,
+                                      T* __restrict__ dy, int lddy, T* __restrict__ dmu, int lddmu,
+                                      T* __restrict__ dsc, int lddsc) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)npix * c) return;
+  const int64_t p = idx / c;
+  const int k = (int)(idx - p * c);
+  const float yv = to_f(y[p * ldy + k]);
+  const float m = to_f(mu[p * ldmu + k]);
+  const float val = (yv + noise_u(seed, (uint64_t)idx)) - m;
+  const float v = fabsf(val);
+  const float scr = to_f(sc[p * ldsc + k]);
+  const float s = fmaxf(scr, sbound);
+  const float cst = -0.70710678118654752440f;
+  const float aa = (0.5f - v) / s, bb = (-0.5f - v) / s;
+  const float L = 0.5f * erfcf(cst * aa) - 0.5f * erfcf(cst * bb);
+  const float Lb = fmaxf(L, lbound);
+  const float dLb = gout[0] * factor / Lb;                       // d(sum ln L') / dL'
+  const float dL = (L >= lbound || dLb < 0.f) ? dLb : 0.f;       // LowerBound(L, 1e-9)
+  const float pa = 0.39894228040143268f * expf(-0.5f * aa * aa);
+  const float pb = 0.39894228040143268f * expf(-0.5f * bb * bb);
+  const float dv = dL * (pb - pa) / s;
+  const float dsv = -dL * (pa * (0.5f - v) + pb * (0.5f + v)) / (s * s);
+  const float ds = (scr >= sbound || dsv < 0.f) ? dsv : 0.f;     // LowerBound(scale, 0.11)
+  const float sgn = val > 0.f ? 1.f : (val < 0.f ? -1.f : 0.f);
+  const float dval = dv * sgn;
+  dy[p * lddy + k] = from_f<T>(dval);
+  dmu[p * lddmu + k] = from_f<T>(-dval);
+  dsc[p * lddsc + k] = from_f<T>(ds);
+}
+
+// ---------------------------------------------------------------------------- recon head (train)
+// x~ = tanh(W_b x16) per image (batch_conv + tanh, net_ga.py:969-979,1092); MSE partials vs the
+// NCHW fp32 image; backward: dpre = g*factor*(x~ - x)(1 - x~^2), dx16 = W_b^T dpre, dW_b partials.
+template <typename T>
+__global__ __launch_bounds__(256) void recon_train_fwd_kernel(const T* __restrict__ x16, int ldx, int hw, int cin,
+                                                              const T* __restrict__ wgen, int ldw,
+                                                              const float* __restrict__ img, float* __restrict__ xt,
+                                                              double* __restrict__ parts) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  double acc = 0.0;
+  if (p < hw) {
+    const T* xr = x16 + ((int64_t)b * hw + p) * ldx;
+    const T* wr = wgen + (int64_t)b * ldw;
+    for (int o = 0; o < 3; ++o) {
+      float v = 0.f;
+      for (int cc = 0; cc < cin; ++cc) v += to_f(wr[o * cin + cc]) * to_f(xr[cc]);
+      const float t = tanhf(v);
+      const int64_t q = ((int64_t)b * 3 + o) * hw + p;
+      if (xt) xt[q] = t;
+      const float e = t - img[q];
+      acc += (double)(e * e);
+    }
+  }
+  const double t = block_sum_f64_256(acc, red);
+  if (threadIdx.x == 0) parts[(int64_t)b * gridDim.x + blockIdx.x] = t;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void recon_train_bwd_kernel(const T* __restrict__ x16, int ldx, int hw, int cin,
+                                                              const T* __restrict__ wgen, int ldw,
+                                                              const float* __restrict__ img,
+                                                              const float* __restrict__ gout, float factor,
+                                                              T* __restrict__ dx16, int lddx,
+                                                              float* __restrict__ wparts) {
+  __shared__ float red[4][48];
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dpre[3] = {0.f, 0.f, 0.f};
+  float xv[16];
+  const bool ok = p < hw;
+  const T* wr = wgen + (int64_t)b * ldw;
+  if (ok) {
+    const T* xr = x16 + ((int64_t)b * hw + p) * ldx;
+    for (int cc = 0; cc < cin; ++cc) xv[cc] = to_f(xr[cc]);
+    const float g = gout[0] * factor;
+    for (int o = 0; o < 3; ++o) {
+      float v = 0.f;
+      for (int cc = 0; cc < cin; ++cc) v += to_f(wr[o * cin + cc]) * xv[cc];
+      const float t = tanhf(v);
+      const int64_t q = ((int64_t)b * 3 + o) * hw + p;
+      dpre[o] = g * (t - img[q]) * (1.f - t * t);
+    }
+    T* dr = dx16 + ((int64_t)b * hw + p) * lddx;
+    for (int cc = 0; cc < cin; ++cc) {
+      float s = 0.f;
+      for (int o = 0; o < 3; ++o) s += to_f(wr[o * cin + cc]) * dpre[o];
+      dr[cc] = from_f<T>(s);
+    }
+  } else {
+    for (int cc = 0; cc < 16; ++cc) xv[cc] = 0.f;
+  }
+  // dW_b[o][cc] partial over this block's pixels
+  for (int k = 0; k < 3 * cin; ++k) {
+    float v = ok ? dpre[k / cin] * xv[k % cin] : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 3 * cin; k += 256)
+    wparts[((int64_t)b * gridDim.x + blockIdx.x) * 3 * cin + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+}
+
+__global__ void recon_wreduce_kernel(const float* __restrict__ wparts, int nblk, int n48, int B,
+                                     float* __restrict__ dw) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * n48) return;
+  const int b = idx / n48, k = idx % n48;
+  float s = 0.f;
+  for (int q = 0; q < nblk; ++q) s += wparts[((int64_t)b * nblk + q) * n48 + k];
+  dw[idx] = s;
+}
+
+// ---------------------------------------------------------------------------- depthwise wgrad
+// dW[c][t] = sum_pix dz[pix, c] * x[pix*s + tap_t, c] (groups = C conv, Syntax_Model's
+// DepthwiseSeparableConv); one thread per (tap, channel) chunk of pixels, partials + reduce.
+template <typename T>
+__global__ void dw_wgrad_kernel(const T* __restrict__ x, int ldx, const T* __restrict__ dz, int ldz, int n, int h,
+                                int w, int ho, int wo, int c, int stride, int ntaps, const DwTaps tp, int per,
+                                float* __restrict__ parts) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // ch * ntaps + t (torch [C, 1, kh, kw] order)
+  if (idx >= ntaps * c) return;
+  const int ch = idx / ntaps, t = idx % ntaps;
+  const int K = n * ho * wo;
+  const int k0 = blockIdx.y * per, k1 = min(K, k0 + per);
+  const int ty = tp.dy[t], tx = tp.dx[t];
+  float s = 0.f;
+  for (int k = k0; k < k1; ++k) {
+    const int b = k / (ho * wo), rem = k % (ho * wo), i = rem / wo, j = rem % wo;
+    const int iy = i * stride + ty, ix = j * stride + tx;
+    if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w)
+      s += to_f(dz[(int64_t)k * ldz + ch]) * to_f(x[(((int64_t)b * h + iy) * w + ix) * ldx + ch]);
+  }
+  parts[(int64_t)blockIdx.y * ntaps * c + idx] = s;
+}
+
+// ---------------------------------------------------------------------------- small elementwise
+// AdaptiveAvgPool2d(1) backward: dx[b, p, c] = dy[b, c] / hw
+template <typename T>
+__global__ void avgpool_bwd_kernel(const T* __restrict__ dy, int lddy, int hw, int c, int64_t total,
+                                   T* __restrict__ dx, int lddx) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int64_t p = idx / c;
+  const int ch = (int)(idx - p * c);
+  dx[p * lddx + ch] = from_f<T>(to_f(dy[(p / hw) * lddy + ch]) / (float)hw);
+}
+
+// y = r + 0.5 tanh(x) (LRP, net_ga.py:1060-1062); backward dx = dy * 0.5 (1 - tanh(x)^2), dr = dy
+template <typename T>
+__global__ void half_tanh_fwd_kernel(const T* __restrict__ x, int ldx, const T* __restrict__ r, int ldr, int npix,
+                                     int c, T* __restrict__ y, int ldy) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)npix * c) return;
+  const int64_t p = idx / c;
+  const int ch = (int)(idx - p * c);
+  y[p * ldy + ch] = from_f<T>(to_f(r[p * ldr + ch]) + 0.5f * tanhf(to_f(x[p * ldx + ch])));
+}
+
+template <typename T>
+__global__ void half_tanh_bwd_kernel(const T* __restrict__ x, int ldx, const T* __restrict__ dy, int lddy, int npix,
+                                     int c, T* __restrict__ dx, int lddx) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)npix * c) return;
+  const int64_t p = idx / c;
+  const int ch = (int)(idx - p * c);
+  const float t = tanhf(to_f(x[p * ldx + ch]));
+  dx[p * lddx + ch] = from_f<T>(to_f(dy[p * lddy + ch]) * 0.5f * (1.f - t * t));
+}
+
 }  // namespace lic
 
 using namespace lic;
@@ -442,7 +921,7 @@ extern "C" int lic_channel_sum(int32_t dtype, const void* x, int32_t ldx, int32_
                                    npix, c, per, ws));
     LIC_CHECK_LAUNCH();
   } else {
-    hipMemsetAsync(ws, 0, (size_t)c * sizeof(float), s);
+    (void)hipMemsetAsync(ws, 0, (size_t)c * sizeof(float), s);
   }
   hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((c + 255) / 256), dim3(256), 0, s, ws, npix > 0 ? nparts : 1, c,
                      out, accumulate);
@@ -516,6 +995,213 @@ extern "C" int lic_lower_bound_sq_bwd(const float* q, const float* dq_eff, int32
   if (count <= 0) return 0;
   hipLaunchKernelGGL(lower_bound_sq_bwd_kernel, dim3(tr_nblk(count)), dim3(256), 0, (hipStream_t)stream, q, dq_eff,
                      count, bound, dq, accumulate);
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t lic_win_attn_bwd_workspace(const lic_attn_args* a) {
+  if (!a || a->ws <= 0 || a->heads <= 0) return -1;
+  const int R = (2 * a->ws - 1) * (2 * a->ws - 1);
+  return (int64_t)a->heads * a->n * (a->h / a->ws) * (a->w / a->ws) * R * (int64_t)sizeof(float);
+}
+
+extern "C" int lic_win_attn_bwd(const lic_attn_args* ap, const void* dout, int32_t lddo, void* dqkv, int32_t lddq,
+                                float* dtable, int32_t accumulate_table, float* ws, int64_t ws_bytes,
+                                lic_stream_t stream) {
+  if (!ap || !ap->qkv || !dout || !dqkv || !ap->table) return fail("attn_bwd: null tensor");
+  const lic_attn_args& a = *ap;
+  if (a.heads <= 0 || a.c % a.heads) return fail("attn_bwd: C % heads != 0");
+  if (a.ws <= 0 || a.h % a.ws || a.w % a.ws) return fail("attn_bwd: H, W must be multiples of the window");
+  if (a.shift < 0 || a.shift >= a.ws) return fail("attn_bwd: 0 <= shift < ws");
+  if ((int64_t)a.n * a.h * a.w == 0) return 0;
+  const int N = a.ws * a.ws, d = a.c / a.heads, R = (2 * a.ws - 1) * (2 * a.ws - 1);
+  const size_t shm = (size_t)(4 * N * (d + 1) + N * (N + 1) + N + R) * sizeof(float);
+  if (shm > 64 * 1024) return fail("attn_bwd: window x head_dim too large for LDS");
+  const int64_t need = lic_win_attn_bwd_workspace(ap);
+  if (dtable && (!ws || ws_bytes < need)) return fail("attn_bwd: workspace too small");
+  const int nwin = a.n * (a.h / a.ws) * (a.w / a.ws);
+  const int64_t blocks = (int64_t)nwin * a.heads;
+  hipStream_t s = (hipStream_t)stream;
+  float* tp = dtable ? ws : nullptr;
+  TR_DISPATCH(a.dtype, "attn_bwd",
+              hipLaunchKernelGGL(win_attn_bwd_kernel<T>, dim3((unsigned)blocks), dim3(256), shm, s, a,
+                                 (const T*)dout, lddo, (T*)dqkv, lddq, tp));
+  LIC_CHECK_LAUNCH();
+  if (dtable) {
+    hipLaunchKernelGGL(attn_table_reduce_kernel, dim3((a.heads * R + 255) / 256), dim3(256), 0, s, ws, a.heads, nwin,
+                       R, dtable, a.tab_sr, a.tab_sh, accumulate_table);
+    LIC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int64_t lic_layernorm_bwd_workspace(int32_t npix, int32_t c) {
+  const int blocks = std::max(1, std::min(1024, (npix + 3) / 4));
+  return (int64_t)blocks * 2 * c * (int64_t)sizeof(float);
+}
+
+extern "C" int lic_layernorm_bwd(int32_t dtype, const void* x, int32_t ldx, const void* dy, int32_t lddy,
+                                 int32_t npix, int32_t c, const float* weight, float eps, void* dx, int32_t lddx,
+                                 float* dwb, int32_t accumulate, float* ws, int64_t ws_bytes, lic_stream_t stream) {
+  if (npix <= 0 || c <= 0) return 0;
+  if (c > 64 * 12) return fail("layernorm_bwd: C > 768");
+  const int blocks = std::max(1, std::min(1024, (npix + 3) / 4));
+  if (ws_bytes < lic_layernorm_bwd_workspace(npix, c)) return fail("layernorm_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int cpl = (c + 63) / 64;
+#define LNB(CPL)                                                                                                  \
+  TR_DISPATCH(dtype, "layernorm_bwd",                                                                            \
+              hipLaunchKernelGGL((layernorm_bwd_kernel<T, CPL>), dim3(blocks), dim3(256), 0, s, (const T*)x, ldx, \
+                                 (const T*)dy, lddy, npix, c, weight, eps, (T*)dx, lddx, ws))
+  if (cpl <= 2) LNB(2);
+  else if (cpl <= 4) LNB(4);
+  else if (cpl <= 8) LNB(8);
+  else LNB(12);
+#undef LNB
+  LIC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((2 * c + 255) / 256), dim3(256), 0, s, ws, blocks, 2 * c, dwb,
+                     accumulate);
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_gate_fwd(int32_t dtype, const void* a, int32_t lda, const void* g, int32_t ldg, const void* r,
+                            int32_t ldr, int32_t npix, int32_t c, void* y, int32_t ldy, lic_stream_t stream) {
+  const int64_t total = (int64_t)npix * c;
+  if (!total) return 0;
+  TR_DISPATCH(dtype, "gate_fwd",
+              hipLaunchKernelGGL(gate_fwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
+                                 (const T*)a, lda, (const T*)g, ldg, (const T*)r, ldr, npix, c, (T*)y, ldy));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int32_t lic_rate_train_parts(int32_t npix, int32_t c) { return (int32_t)tr_nblk((int64_t)npix * c); }
+
+extern "C" int lic_rate_train_fwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
+                                  const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                                  float scale_bound, float likelihood_bound, void* yhat, int32_t ldyh,
+                                  double* partials, lic_stream_t stream) {
+  const int64_t total = (int64_t)npix * c;
+  if (!total) return 0;
+  TR_DISPATCH(dtype, "rate_train_fwd",
+              hipLaunchKernelGGL(rate_train_fwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
+                                 (const T*)y, ldy, (const T*)mu, ldmu, (const T*)scale, ldsc, npix, c, seed,
+                                 scale_bound, likelihood_bound, (T*)yhat, ldyh, partials));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_rate_train_bwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
+                                  const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                                  float scale_bound, float likelihood_bound, const float* gout, float factor,
+                                  void* dy, int32_t lddy, void* dmu, int32_t lddmu, void* dscale, int32_t lddsc,
+                                  lic_stream_t stream) {
+  const int64_t total = (int64_t)npix * c;
+  if (!total) return 0;
+  TR_DISPATCH(dtype, "rate_train_bwd",
+              hipLaunchKernelGGL(rate_train_bwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
+                                 (const T*)y, ldy, (const T*)mu, ldmu, (const T*)scale, ldsc, npix, c, seed,
+                                 scale_bound, likelihood_bound, gout, factor, (T*)dy, lddy, (T*)dmu, lddmu,
+                                 (T*)dscale, lddsc));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int32_t lic_recon_train_blocks(int32_t hw) { return (hw + 255) / 256; }
+
+extern "C" int lic_recon_train_fwd(int32_t dtype, const void* x16, int32_t ldx, int32_t n, int32_t hw, int32_t cin,
+                                   const void* wgen, int32_t ldw, const float* img, float* xt, double* partials,
+                                   lic_stream_t stream) {
+  if (cin > 16 || cin <= 0) return fail("recon_train: cin must be 1..16");
+  if (n <= 0 || hw <= 0) return 0;
+  dim3 grid((hw + 255) / 256, n);
+  TR_DISPATCH(dtype, "recon_train_fwd",
+              hipLaunchKernelGGL(recon_train_fwd_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)x16,
+                                 ldx, hw, cin, (const T*)wgen, ldw, img, xt, partials));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_recon_train_bwd(int32_t dtype, const void* x16, int32_t ldx, int32_t n, int32_t hw, int32_t cin,
+                                   const void* wgen, int32_t ldw, const float* img, const float* gout, float factor,
+                                   void* dx16, int32_t lddx, float* dw, float* ws, int64_t ws_bytes,
+                                   lic_stream_t stream) {
+  if (cin > 16 || cin <= 0) return fail("recon_train: cin must be 1..16");
+  if (n <= 0 || hw <= 0) return 0;
+  const int nblk = (hw + 255) / 256;
+  if (ws_bytes < (int64_t)n * nblk * 3 * cin * (int64_t)sizeof(float)) return fail("recon_train_bwd: workspace");
+  hipStream_t s = (hipStream_t)stream;
+  TR_DISPATCH(dtype, "recon_train_bwd",
+              hipLaunchKernelGGL(recon_train_bwd_kernel<T>, dim3(nblk, n), dim3(256), 0, s, (const T*)x16, ldx, hw,
+                                 cin, (const T*)wgen, ldw, img, gout, factor, (T*)dx16, lddx, ws));
+  LIC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(recon_wreduce_kernel, dim3((n * 3 * cin + 255) / 256), dim3(256), 0, s, ws, nblk, 3 * cin, n,
+                     dw);
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t lic_dwconv_wgrad_workspace(int32_t n, int32_t ho, int32_t wo, int32_t c, int32_t ntaps) {
+  const int K = n * ho * wo;
+  const int nsplit = std::max(1, std::min(256, K / 64));
+  return (int64_t)nsplit * ntaps * c * (int64_t)sizeof(float);
+}
+
+extern "C" int lic_avgpool_bwd(int32_t dtype, const void* dy, int32_t lddy, int32_t n, int32_t hw, int32_t c,
+                               void* dx, int32_t lddx, lic_stream_t stream) {
+  const int64_t total = (int64_t)n * hw * c;
+  if (!total) return 0;
+  TR_DISPATCH(dtype, "avgpool_bwd",
+              hipLaunchKernelGGL(avgpool_bwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
+                                 (const T*)dy, lddy, hw, c, total, (T*)dx, lddx));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_half_tanh_fwd(int32_t dtype, const void* x, int32_t ldx, const void* r, int32_t ldr, int32_t npix,
+                                 int32_t c, void* y, int32_t ldy, lic_stream_t stream) {
+  const int64_t total = (int64_t)npix * c;
+  if (!total) return 0;
+  TR_DISPATCH(dtype, "half_tanh_fwd",
+              hipLaunchKernelGGL(half_tanh_fwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
+                                 (const T*)x, ldx, (const T*)r, ldr, npix, c, (T*)y, ldy));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_half_tanh_bwd(int32_t dtype, const void* x, int32_t ldx, const void* dy, int32_t lddy,
+                                 int32_t npix, int32_t c, void* dx, int32_t lddx, lic_stream_t stream) {
+  const int64_t total = (int64_t)npix * c;
+  if (!total) return 0;
+  TR_DISPATCH(dtype, "half_tanh_bwd",
+              hipLaunchKernelGGL(half_tanh_bwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
+                                 (const T*)x, ldx, (const T*)dy, lddy, npix, c, (T*)dx, lddx));
+  LIC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int lic_dwconv_wgrad(int32_t dtype, const void* x, int32_t ldx, const void* dz, int32_t ldz, int32_t n,
+                                int32_t h, int32_t w, int32_t ho, int32_t wo, int32_t c, int32_t stride,
+                                int32_t ntaps, const int8_t* dy_host, const int8_t* dx_host, float* dw, float* ws,
+                                int64_t ws_bytes, lic_stream_t stream) {
+  if (ntaps <= 0 || ntaps > LIC_MAX_TAPS) return fail("dwconv_wgrad: ntaps");
+  const int K = n * ho * wo;
+  if (K <= 0) return 0;
+  const int nsplit = std::max(1, std::min(256, K / 64));
+  const int per = (K + nsplit - 1) / nsplit;
+  const int64_t need = (int64_t)nsplit * ntaps * c * (int64_t)sizeof(float);
+  if (ws_bytes < need) return fail("dwconv_wgrad: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  DwTaps tp;
+  for (int t = 0; t < ntaps; ++t) { tp.dy[t] = dy_host[t]; tp.dx[t] = dx_host[t]; }
+  dim3 grid((ntaps * c + 255) / 256, nsplit);
+  TR_DISPATCH(dtype, "dwconv_wgrad",
+              hipLaunchKernelGGL(dw_wgrad_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ldx, (const T*)dz, ldz, n, h,
+                                 w, ho, wo, c, stride, ntaps, tp, per, ws));
+  LIC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((ntaps * c + 255) / 256), dim3(256), 0, s, ws, nsplit,
+                     ntaps * c, dw, 0);
   LIC_CHECK_LAUNCH();
   return 0;
 }

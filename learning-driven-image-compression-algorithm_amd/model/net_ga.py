@@ -696,13 +696,25 @@ class Net(nn.Module):
         Fn.recon(xh, cwh, 0, post=post[1], x=x_in, x_rec=x_rec, parts=sq_parts, ppi=ppi)   # :1099-1100
 
     # ---- forward
-    @torch.no_grad()
-    def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False):
+    def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False,
+                seed: Optional[int] = None):
+        """mode='test': (bpp, v_mse, v_psnr) (eval semantics, no autograd).  mode='train':
+        (bpp, mse) differentiable through liblic (lic_amd/train_net.py); ``seed`` picks the
+        GaussianConditional noise stream (default: a per-module counter)."""
         if not inputs.is_cuda:
             raise RuntimeError("lic_amd Net runs on the GPU only (HIP path); move inputs to cuda")
+        if mode == 'train':
+            from ..train_net import net_forward_train
+            if seed is None:
+                seed = self.__dict__.get("_train_calls", 0)
+                self.__dict__["_train_calls"] = seed + 1
+            return net_forward_train(self, inputs, seed)
         if mode != 'test':
-            raise NotImplementedError("mode='train' needs the backward kernels (SURVEY.md 8(f) rank 1); "
-                                      "use mode='test'")
+            raise ValueError(f"mode must be 'train' or 'test', got {mode!r}")
+        with torch.no_grad():
+            return self._forward_test(inputs, return_intermediates)
+
+    def _forward_test(self, inputs: torch.Tensor, return_intermediates: bool):
         b, h, w, c = self.train_size
         x_in = inputs.contiguous().float()
         B, _, H, W = x_in.shape

@@ -182,3 +182,174 @@ def test_wgrad_large_k(dtype):
     AG.wgrad(x.to(DEV), dz.to(DEV), tdy, tdx, dw=dw, strides=(64 * 9, 9, 1), co_out=64, ci_out=64)
     ref = torch.nn.grad.conv2d_weight(_nchw(x), (64, 64, 3, 3), _nchw(dz), padding=1)
     _rel(dw, ref, dtype, "dw")
+
+
+# --------------------------------------------------------------------------- ops of the full training graph
+class _LBFn(torch.autograd.Function):
+    """ops/bound_ops.py:25-28 LowerBound gradient rule (pass if x >= bound or grad < 0)."""
+
+    @staticmethod
+    def forward(ctx, v, bound):
+        ctx.save_for_backward(v)
+        ctx.bound = bound
+        return torch.clamp(v, min=bound)
+
+    @staticmethod
+    def backward(ctx, go):
+        (v,) = ctx.saved_tensors
+        return ((v >= ctx.bound) | (go < 0)).to(go.dtype) * go, None
+
+
+def _check(gpu_fn, ref_fn, tensors, act, dtype, seed=0):
+    """Forward outputs and input grads of gpu_fn vs the fp32 CPU autograd of ref_fn; tensors are CPU
+    fp32, act[i] says whether input i is an activation (cast to dtype) or an fp32 parameter."""
+    g = torch.Generator().manual_seed(seed)
+    rs = [t.clone().requires_grad_(True) for t in tensors]
+    outs_r = ref_fn(*rs)
+    outs_r = outs_r if isinstance(outs_r, tuple) else (outs_r,)
+    gs = [torch.randn(o.shape, generator=g) for o in outs_r]
+    torch.autograd.backward(outs_r, gs)
+    gt = [t.to(DEV, dtype if a else torch.float32).requires_grad_(True) for t, a in zip(tensors, act)]
+    outs_g = gpu_fn(*gt)
+    outs_g = outs_g if isinstance(outs_g, tuple) else (outs_g,)
+    torch.autograd.backward(outs_g, [gg.to(DEV, o.dtype) for gg, o in zip(gs, outs_g)])
+    torch.cuda.synchronize()
+    for i, (o, r) in enumerate(zip(outs_g, outs_r)):
+        _rel(o, r, dtype, f"out{i}")
+    for i, (a_, r) in enumerate(zip(gt, rs)):
+        if r.grad is not None:
+            _rel(a_.grad, r.grad, dtype, f"grad{i}")
+
+
+def _attn_core_ref(qkv, table, C, heads, ws, shift, wmsa):
+    """WBA (layers/win_attention.py:85-116, 154-209) / WMSA (model/Block_unet.py:216-252) attention
+    core from a qkv map, written with the oracle's window helpers."""
+    from oracle import ref_cpu as R
+    B, H, W, _ = qkv.shape
+    d, N = C // heads, ws * ws
+    x = torch.roll(qkv, (-shift, -shift), (1, 2)) if shift else qkv
+    t = R.window_partition(x, ws).view(-1, N, 3, heads, d).permute(2, 0, 3, 1, 4)
+    q, k, v = t[0], t[1], t[2]
+    scale = d ** -0.5
+    attn = (q @ k.transpose(-2, -1)) * scale if wmsa else (q * scale) @ k.transpose(-2, -1)
+    rpi = R.relative_position_index(ws).view(-1)
+    rpb = table.reshape(heads, -1)[:, rpi].view(heads, N, N) if wmsa else table[rpi].view(N, N, heads).permute(2, 0, 1)
+    attn = attn + rpb.unsqueeze(0)
+    nW = (H // ws) * (W // ws)
+    if shift and not wmsa:
+        attn = (attn.view(B, nW, heads, N, N) + R.wba_mask(H, W, ws, shift).unsqueeze(1).unsqueeze(0)).view(-1, heads, N, N)
+    if shift and wmsa:
+        m = R.wmsa_mask(H // ws, W // ws, ws, shift)
+        attn = attn.view(B, nW, heads, N, N).masked_fill(m.unsqueeze(0).unsqueeze(2), float("-inf")).view(-1, heads, N, N)
+    o = (torch.softmax(attn, -1) @ v).transpose(1, 2).reshape(-1, ws, ws, C)
+    o = R.window_reverse(o, ws, H, W)
+    return torch.roll(o, (shift, shift), (1, 2)) if shift else o
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("ws,shift,wmsa,C", [(8, 4, False, 192), (8, 0, False, 64), (4, 2, False, 64),
+                                             (2, 1, False, 64), (8, 4, True, 128), (8, 0, True, 128)])
+def test_win_attn_grad(dtype, ws, shift, wmsa, C):
+    from lic_amd import autograd as AG
+    heads = 8
+    g = torch.Generator().manual_seed(ws * 10 + shift + C)
+    qkv = torch.randn(2, 16, 16, 3 * C, generator=g)
+    R_ = (2 * ws - 1) ** 2
+    table = (torch.randn(heads, 2 * ws - 1, 2 * ws - 1, generator=g) if wmsa else torch.randn(R_, heads, generator=g))
+    table = table * 0.5
+    _check(lambda x, t: AG.win_attn(x, t, C, heads, ws, shift, tab_sr=1 if wmsa else heads, tab_sh=R_ if wmsa else 1,
+                                    mask_kind=(2 if wmsa else 1) if shift else 0, scale_after=wmsa,
+                                    scale=(C // heads) ** -0.5),
+           lambda x, t: _attn_core_ref(x, t, C, heads, ws, shift, wmsa), [qkv, table], [True, False], dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("C", [128, 192])
+def test_layernorm_grad(dtype, C):
+    from lic_amd import autograd as AG
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(2, 8, 8, C, generator=g) * 2 + 0.5
+    w = 1 + 0.1 * torch.randn(C, generator=g)
+    b = 0.1 * torch.randn(C, generator=g)
+    _check(lambda x_, w_, b_: AG.layernorm(x_, w_, b_, 1e-5), lambda x_, w_, b_: F.layer_norm(x_, (C,), w_, b_, 1e-5),
+           [x, w, b], [True, False, False], dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_elementwise_grads(dtype):
+    from lic_amd import autograd as AG
+    g = torch.Generator().manual_seed(1)
+    a, b, r = (torch.randn(2, 6, 7, 48, generator=g) for _ in range(3))
+    _check(AG.gate, lambda b_, a_, r_: a_ * torch.sigmoid(b_) + r_, [b, a, r], [True] * 3, dtype)
+    _check(AG.half_tanh_add, lambda x_, r_: r_ + 0.5 * torch.tanh(x_), [a, r], [True] * 2, dtype)
+    _check(AG.add, lambda x_, y_: x_ + y_, [a, b], [True] * 2, dtype)
+    _check(AG.avgpool, lambda x_: x_.mean((1, 2), keepdim=True), [a], [True], dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_dwconv_grad(dtype):
+    from lic_amd import autograd as AG
+    g = torch.Generator().manual_seed(2)
+    C = 32
+    x = torch.randn(2, 16, 16, C, generator=g)
+    w = torch.randn(C, 1, 3, 3, generator=g) / 3
+    b = 0.1 * torch.randn(C, generator=g)
+    _check(lambda x_, w_, b_: AG.dwconv2d(x_, w_, b_, 1, 1),
+           lambda x_, w_, b_: F.conv2d(x_.permute(0, 3, 1, 2), w_, b_, 1, 1, 1, C).permute(0, 2, 3, 1),
+           [x, w, b], [True, False, False], dtype)
+
+
+def _noise_ref(seed, n):
+    """The rate kernels' counter-based U(-1/2, 1/2) noise (train.hip noise_u), restated in numpy."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint64)
+        z = np.array([seed], dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + i
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    u = (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0) - np.float32(0.5)
+    return torch.from_numpy(u)
+
+
+def _rate_ref(y, mu, sc, seed, num_pixels):
+    """compressai GaussianConditional.forward in training mode (noise) + LowerBound rules, and
+    ste_round(y - mu) + mu (net_ga.py:1049-1053); y, mu, sc NHWC."""
+    import math
+    u = _noise_ref(seed, y.numel()).view(y.shape)
+    v = ((y + u) - mu).abs()
+    s = _LBFn.apply(sc, 0.11)
+    c = -(2 ** -0.5)
+    L = 0.5 * torch.erfc(c * ((0.5 - v) / s)) - 0.5 * torch.erfc(c * ((-0.5 - v) / s))
+    L = _LBFn.apply(L, 1e-9)
+    bpp = torch.log(L).sum() / (-math.log(2) * num_pixels)
+    d = y - mu
+    return bpp, (torch.round(d) - d.detach() + d) + mu
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_rate_train_grad(dtype):
+    from lic_amd import autograd as AG
+    g = torch.Generator().manual_seed(5)
+    y = torch.randn(2, 8, 8, 48, generator=g) * 3
+    mu = torch.randn(2, 8, 8, 48, generator=g)
+    sc = torch.rand(2, 8, 8, 48, generator=g) * 2 - 0.2     # some scales under the 0.11 bound
+    if dtype == torch.float16:   # the reference sees the same fp16-rounded inputs
+        y, mu, sc = y.half().float(), mu.half().float(), sc.half().float()
+    _check(lambda a, b, c: AG.rate_train(a, b, c, 77, 2 * 128 * 128),
+           lambda a, b, c: _rate_ref(a, b, c, 77, 2 * 128 * 128), [y, mu, sc], [True] * 3, dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_recon_mse_grad(dtype):
+    from lic_amd import autograd as AG
+    g = torch.Generator().manual_seed(6)
+    x16 = torch.randn(2, 32, 32, 16, generator=g) * 0.5
+    cw = torch.randn(2, 1, 1, 48, generator=g) * 0.3
+    img = torch.rand(2, 3, 32, 32, generator=g) * 2 - 1
+
+    def ref(x_, w_):
+        xt = torch.tanh(torch.einsum("bhwc,boc->bohw", x_, w_.view(2, 3, 16)))
+        return ((xt - img) ** 2).mean()
+
+    _check(lambda x_, w_: AG.recon_mse(x_, w_, img.to(DEV)), ref, [x16, cw], [True, True], dtype)
