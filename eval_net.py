@@ -7,7 +7,8 @@ unsynchronised, :93-100); no PNG side effects; ``--all-images`` evaluates every 
 (the reference only evaluates ``sorted(glob)[22:23]``, :31); ``--arch`` / ``--precision``
 select the model file and the activation dtype; a missing checkpoint falls back to the
 reference's seeded initialisation with a warning (no checkpoints ship with the reference).
-``--pre_processing`` (online finetune) needs the training path and is not available yet.
+``--pre_processing`` runs the online encoder finetune (eval_net.py:118-199) on the liblic training
+path (Net.forward(x, 'train') + backward) before evaluating each image.
 
 BASELINE config 4 (Kodak-24 R-D sweep, image-sharded over 1/2/4/8 GPUs):
 ``--synthetic-kodak`` stands in for the Kodak PNGs (none ship with the reference and
@@ -151,11 +152,25 @@ def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=Fals
     return summaries, n_img / elapsed, world
 
 
+def finetune_encoder(net, data, lmbda, tune_iter):
+    """Online encoder finetune (eval_net.py:160-179): Adam(a_model, 1e-5), MultiStepLR([50], 0.5),
+    loss = lambda * mse + bpp in train mode, post-processing off during the finetune."""
+    opt_enc = torch.optim.Adam(net.a_model.parameters(), lr=1e-5)
+    sch = torch.optim.lr_scheduler.MultiStepLR(opt_enc, [50], 0.5)
+    post = net.post_processing
+    net.post_processing = False
+    for _ in range(tune_iter):
+        train_bpp, train_mse = net(data, 'train')
+        train_loss = (lmbda * train_mse + train_bpp).mean()
+        opt_enc.zero_grad()
+        train_loss.backward()
+        opt_enc.step()
+        sch.step()
+    net.post_processing = post
+
+
 def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing, tune_iter, arch="net_ga",
         precision="fp32", all_images=False, device="cuda"):
-    if pre_processing:
-        raise NotImplementedError("--pre_processing (online encoder finetune) needs the training path "
-                                  "(SURVEY.md 8(f) rank 4)")
     from lic_amd.model import net_ga, net_unet_ha_hs
     from lic_amd import distributed as D
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
@@ -184,6 +199,8 @@ def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing,
             print(f"warning: checkpoint {weight_path!r} not found; using the seeded reference initialisation")
         torch.cuda.synchronize()
         begin_time = time.time()
+        if pre_processing:
+            finetune_encoder(net, data, lmbda, tune_iter)
         with torch.no_grad():
             eval_bpp, v_mse, v_psnr = net(data, 'test')
         torch.cuda.synchronize()
@@ -197,7 +214,9 @@ def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing,
         cnt += 1
     sum_time, list_eval_bpp, list_v_psnr, list_v_mse, cnt = D.sum_over_ranks(
         [sum_time, list_eval_bpp, list_v_psnr, list_v_mse, cnt], world, device)
-    if cnt and rank == 0:
+    if cnt and rank == 0 and pre_processing:
+        print('[WITH PRE-PROCESSING] bpp: %.4f psnr: %.4f' % (list_eval_bpp / cnt, list_v_psnr / cnt))
+    elif cnt and rank == 0:
         print('[WITHOUT PRE-PROCESSING] ave_time:%.4f bpp: %.4f psnr: %.4f  v_mse: %.4f' % (
             sum_time / cnt, list_eval_bpp / cnt, list_v_psnr / cnt, list_v_mse / cnt))
     D.finish(world)

@@ -67,3 +67,73 @@ def finish(world: int) -> None:
     if world > 1 and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+class GradAllReduce:
+    """Data-parallel gradient averaging for the training path (replaces the
+    reference's single-process ``nn.DataParallel`` gradient sum, train_net_unet.py:152).
+
+    One process per GPU; parameters are grouped into ~``bucket_mb`` buckets in reverse
+    registration order (roughly the order backward produces their gradients).  A
+    post-accumulate-grad hook counts each bucket down; when its last gradient lands the
+    bucket is flattened and an async all-reduce (SUM) is launched on it (RCCL over xGMI),
+    overlapping the rest of the backward.  ``finish()`` launches what is left (buckets
+    holding parameters that got no gradient this step: only the ones that did are reduced,
+    the same set on every rank because every rank runs the same graph), waits, divides by
+    the world size and scatters back into ``.grad``."""
+
+    def __init__(self, params, world: int, bucket_mb: float = 32.0):
+        self.world = world
+        self.params = [p for p in params if p.requires_grad]
+        buckets, cur, size = [], [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * 4
+            if size >= bucket_mb * 2 ** 20:
+                buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            buckets.append(cur)
+        self.buckets = buckets
+        self._where = {id(p): i for i, b in enumerate(buckets) for p in b}
+        self._pending = [len(b) for b in buckets]
+        self._work = [None] * len(buckets)
+        self._flat = [None] * len(buckets)
+        self._members = [None] * len(buckets)
+        self._hooks = []
+        if world > 1:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p):
+        i = self._where[id(p)]
+        self._pending[i] -= 1
+        if self._pending[i] == 0:
+            self._launch(i)
+
+    def _launch(self, i):
+        members = [p for p in self.buckets[i] if p.grad is not None]
+        self._members[i] = members
+        if not members:
+            return
+        flat = torch.cat([p.grad.reshape(-1).float() for p in members])
+        self._flat[i] = flat
+        self._work[i] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)
+
+    def finish(self) -> None:
+        """Complete every bucket's all-reduce and write the averaged gradients back."""
+        if self.world <= 1:
+            return
+        for i in range(len(self.buckets)):
+            if self._members[i] is None:
+                self._launch(i)
+            if self._work[i] is not None:
+                self._work[i].wait()
+                flat = self._flat[i].div_(self.world)
+                off = 0
+                for p in self._members[i]:
+                    n = p.numel()
+                    p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                    off += n
+            self._pending[i] = len(self.buckets[i])
+            self._work[i] = self._flat[i] = self._members[i] = None

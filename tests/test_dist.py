@@ -63,3 +63,59 @@ def test_single_process_is_identity():
     assert D.shard([1, 2, 3], 0, 1) == [1, 2, 3]
     assert D.sum_over_ranks([1.0, 2.0], 1) == [1.0, 2.0]
     assert D.max_over_ranks(3.0, 1) == 3.0
+
+
+def _ddp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    D.init("gloo")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    unused = torch.nn.Linear(3, 3)                   # never receives a gradient
+    params = list(model.parameters()) + list(unused.parameters())
+    sync = D.GradAllReduce(params, world, bucket_mb=1e-4)   # tiny buckets: several in flight
+    for step in range(2):
+        for p in params:
+            p.grad = None
+        x = torch.randn(6, 8, generator=torch.Generator().manual_seed(100 * step + rank))
+        model(x).pow(2).sum().backward()
+        sync.finish()
+    q.put((rank, [None if p.grad is None else p.grad.clone() for p in params]))
+    D.finish(world)
+
+
+def test_world2_grad_allreduce_gloo():
+    """Bucketed gradient all-reduce of the training path: both ranks end with the mean of the
+    per-rank gradients; parameters without a gradient stay None."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 4))
+    grads = []
+    for r in range(world):
+        model.zero_grad()
+        x = torch.randn(6, 8, generator=torch.Generator().manual_seed(100 + r))
+        model(x).pow(2).sum().backward()
+        grads.append([p.grad.clone() for p in model.parameters()])
+    mean = [(a + b) / 2 for a, b in zip(*grads)]
+    for r in range(world):
+        got = out[r]
+        for g_, m_ in zip(got[:4], mean):
+            torch.testing.assert_close(g_, m_, rtol=1e-5, atol=1e-6)
+        assert got[4] is None and got[5] is None
+
+
+def test_grad_allreduce_single_process_noop():
+    p = torch.nn.Parameter(torch.ones(3))
+    p.grad = torch.full((3,), 2.0)
+    D.GradAllReduce([p], 1).finish()
+    assert torch.equal(p.grad, torch.full((3,), 2.0))

@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""train_net_unet.py — the reference training CLI (train_net_unet.py:90-238, BASELINE config 5)
+on the liblic training path.
+
+What it does per step, as the reference (:167-200): ``bpp, mse = net(x, 'train')``;
+``loss = lambda * 255**2 * mse + bpp``; backward; ``clip_grad_norm_(params, 1)``;
+``Adam(base_params)`` step; ``MultiStepLR([1500, 2500, 3500, 4000], 0.5)`` per epoch.
+
+Differences:
+  * the model is net_ga (eval_net.py's model): the reference script's ``model/Net_unet.py``
+    imports the missing ``model/Block.py`` and cannot be built;
+  * one process per GPU (``torch.distributed.run``) with a bucketed gradient all-reduce
+    overlapped with the backward (lic_amd.distributed.GradAllReduce, RCCL over xGMI)
+    instead of single-process ``nn.DataParallel`` (:152);
+  * data: no DIV2K and no network here — ``--synthetic`` (default) draws random 256x256
+    crops from a seeded bank of smooth synthetic images resident in HBM;
+  * fp16 activations (fp32 master weights, fp32 accumulation) use a dynamic loss scale
+    (torch.amp.GradScaler); ``--precision fp32`` is the parity path;
+  * the NaN check (:189-190) runs every ``--log_every`` steps instead of syncing each step.
+
+``--bench``: W warm-up + K timed steps between barriers + device syncs; rank 0 prints one
+JSON line (images/s of the whole job, MAX step time over ranks).
+"""
+import argparse
+import json
+import math
+import os
+import random
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def synthetic_bank(n, size, seed, device):
+    from eval_net import synthetic_image
+    return torch.stack([synthetic_image(seed + i, size, size) for i in range(n)]).to(device) * 2 - 1
+
+
+class Crops:
+    """RandomCrop(crop) + Preprocess ([-1, 1]) over an HBM-resident image bank (:24-51)."""
+
+    def __init__(self, bank, batch, crop, seed):
+        self.bank, self.batch, self.crop = bank, batch, crop
+        self.rng = random.Random(seed)
+
+    def __call__(self):
+        n, _, H, W = self.bank.shape
+        out = []
+        for _ in range(self.batch):
+            i = self.rng.randrange(n)
+            y, x = self.rng.randrange(H - self.crop + 1), self.rng.randrange(W - self.crop + 1)
+            out.append(self.bank[i, :, y:y + self.crop, x:x + self.crop])
+        return torch.stack(out).contiguous()
+
+
+def main():
+    ap = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    ap.add_argument("--train_data_path", default="", help="unused: no dataset ships; see --synthetic")
+    ap.add_argument("--weight_path", default="", help="Path of Pretrained Checkpoint")
+    ap.add_argument("--checkpoint_dir", default="", help="Directory of Saved Checkpoints ('' = do not save)")
+    ap.add_argument("--high", action="store_true", help="Using High Bitrate Model")
+    ap.add_argument("--post_processing", action="store_true", help="Using Post Processing (not trainable yet)")
+    ap.add_argument("--lambda", type=float, default=0.0025, dest="lmbda")
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--batch_size", type=float, default=8, help="images per GPU")
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--crop", type=int, default=256)
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--steps_per_epoch", type=int, default=20)
+    ap.add_argument("--log_every", type=int, default=10)
+    ap.add_argument("--bench", action="store_true", help="time --steps steps after --warmup, print JSON")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gpus", type=int, default=1, help="informational; world size comes from torchrun")
+    args = ap.parse_args()
+
+    from lic_amd import distributed as D
+    from lic_amd.model import net_ga
+    rank, world, local = D.init("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B = int(args.batch_size)
+
+    torch.manual_seed(0)
+    net = net_ga.Net((B, args.crop, args.crop, 3), (1, args.crop, args.crop, 3), args.high, args.post_processing,
+                     precision=args.precision)
+    if args.weight_path:
+        net.load_state_dict(torch.load(args.weight_path, map_location="cpu", weights_only=True), strict=True)
+    net = net.to(dev)
+    params = net.base_params()
+    opt = torch.optim.Adam(params, lr=args.lr)
+    sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1500, 2500, 3500, 4000], 0.5)
+    sync = D.GradAllReduce(params, world)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 10, enabled=args.precision == "fp16")
+    batches = Crops(synthetic_bank(16, 2 * args.crop, 5000 + 97 * rank, dev), B, args.crop, 1234 + rank)
+
+    def step():
+        x = batches()
+        opt.zero_grad(set_to_none=True)
+        bpp, mse = net(x, "train")
+        loss = args.lmbda * 255 ** 2 * mse + bpp                       # :180
+        scaler.scale(loss).backward()
+        sync.finish()
+        scaler.unscale_(opt)
+        torch.nn.utils.clip_grad_norm_([p for p in params if p.grad is not None], 1.0)   # :198
+        scaler.step(opt)
+        scaler.update()
+        return loss.detach(), bpp.detach(), mse.detach()
+
+    if args.bench:
+        first = None
+        for _ in range(max(1, args.warmup)):
+            out = step()
+            first = first if first is not None else float(out[0])
+        D.barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        D.barrier(world)
+        dt = D.max_over_ranks(dt, world, dev)
+        last = float(out[0])
+        if rank == 0:
+            print(json.dumps({
+                "metric": f"train images/sec ({args.crop}x{args.crop} crops, net_ga, batch {B}/GPU)",
+                "value": round(world * B * args.steps / dt, 2), "unit": "images/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "f16" if args.precision == "fp16" else "f32",
+                "data": "synthetic (seeded smooth images, random crops in HBM; no DIV2K)",
+                "config": {"workload": "net_ga Net.forward(x,'train') + backward + grad all-reduce + clip + Adam",
+                           "global_batch": world * B, "crop": args.crop, "lambda": args.lmbda,
+                           "parallelism": f"data-parallel x{world} (bucketed RCCL all-reduce)"},
+                "loss_first_last": [round(first, 4), round(last, 4)]}), flush=True)
+        D.finish(world)
+        return
+
+    for epoch in range(args.epochs):
+        sums = [0.0, 0.0, 0.0]
+        acc = None
+        for i in range(args.steps_per_epoch):
+            out = torch.stack(step())
+            acc = out if acc is None else acc + out
+            if (i + 1) % args.log_every == 0 or i + 1 == args.steps_per_epoch:
+                vals = acc.tolist()                                      # one sync per log window
+                if math.isnan(vals[0]):
+                    raise Exception("NaN in loss")                      # :189-190
+                sums = [s + v for s, v in zip(sums, vals)]
+                acc = None
+        sch.step()
+        cnt = args.steps_per_epoch
+        if rank == 0:
+            msg = "[Epoch %04d TRAIN] Loss: %.4f bpp: %.4f mse: %.4f  " % (epoch, sums[0] / cnt, sums[1] / cnt,
+                                                                          sums[2] / cnt)
+            print(msg, flush=True)
+            if args.checkpoint_dir:
+                os.makedirs(args.checkpoint_dir, exist_ok=True)
+                with open(os.path.join(args.checkpoint_dir, "train_log.txt"), "a") as fd:
+                    fd.write(msg + "\n")
+                if epoch % 100 == 99:
+                    torch.save(net.state_dict(), "%s/%04d.ckpt" % (args.checkpoint_dir, epoch))
+    D.finish(world)
+
+
+if __name__ == "__main__":
+    main()
