@@ -196,8 +196,16 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, in
   const int t = (int)(r / co_out);
   const int64_t stride = (int64_t)ntaps * co * ci;
   const float* p = ws + ((int64_t)t * co + n) * ci + c;
-  float s = 0.f;
-  for (int k = 0; k < nsplit; ++k) s += p[k * stride];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= nsplit; k += 4) {
+    s0 += p[k * stride];
+    s1 += p[(k + 1) * stride];
+    s2 += p[(k + 2) * stride];
+    s3 += p[(k + 3) * stride];
+  }
+  for (; k < nsplit; ++k) s0 += p[k * stride];
+  const float s = (s0 + s1) + (s2 + s3);
   float* o = dw + n * s_co + c * s_ci + t * s_tap;
   *o = accumulate ? *o + s : s;
 }
@@ -218,7 +226,7 @@ static WgPlan wgrad_plan(const lic_wgrad_args& a) {
   const int per_split = p.tiles_m * p.tiles_n * a.ntaps;
   const int max_split = std::max(1, (p.K + 8 * bk - 1) / (8 * bk));  // >= 8 K steps per work-group
   int ns = std::max(1, (2048 + per_split - 1) / per_split);
-  ns = std::min(std::min(ns, max_split), 4096);
+  ns = std::min(std::min(ns, max_split), 64);
   int chunk = (p.K + ns - 1) / ns;
   chunk = (chunk + bk - 1) / bk * bk;
   p.nsplit = std::max(1, (p.K + chunk - 1) / chunk);
@@ -255,26 +263,44 @@ static void wgrad_launch(const lic_wgrad_args& a, const WgPlan& p, hipStream_t s
 }
 
 // ---------------------------------------------------------------------------- channel sums
+// Both passes use 64 channels x 4 row groups per 256-thread block (lane = channel, coalesced
+// 128-256 B rows; the 4 groups are folded in LDS), so no thread walks a long serial chain.
 constexpr int CS_CHUNKS = 256;
 
 template <typename T>
-__global__ void channel_sum_partial_kernel(const T* __restrict__ x, int ld, int npix, int c, int per,
-                                           float* __restrict__ parts) {
+__global__ __launch_bounds__(256) void channel_sum_partial_kernel(const T* __restrict__ x, int ld, int npix, int c,
+                                                                  int per, float* __restrict__ parts) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int ch = blockIdx.y * 64 + lane;
   const int p0 = blockIdx.x * per, p1 = min(npix, p0 + per);
-  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
-    float s = 0.f;
-    for (int p = p0; p < p1; ++p) s += to_f(x[(int64_t)p * ld + ch]);
-    parts[(int64_t)blockIdx.x * c + ch] = s;
+  float s = 0.f;
+  if (ch < c)
+    for (int p = p0 + r; p < p1; p += 4) s += to_f(x[(int64_t)p * ld + ch]);
+  red[r][lane] = s;
+  __syncthreads();
+  if (r == 0 && ch < c) parts[(int64_t)blockIdx.x * c + ch] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
+__global__ __launch_bounds__(256) void channel_sum_reduce_kernel(const float* __restrict__ parts, int nparts, int c,
+                                                                 float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (ch < c)
+    for (int k = r; k < nparts; k += 4) s += parts[(int64_t)k * c + ch];
+  red[r][lane] = s;
+  __syncthreads();
+  if (r == 0 && ch < c) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[ch] = accumulate ? out[ch] + t : t;
   }
 }
 
-__global__ void channel_sum_reduce_kernel(const float* __restrict__ parts, int nparts, int c, float* __restrict__ out,
-                                          int accumulate) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  float s = 0.f;
-  for (int k = 0; k < nparts; ++k) s += parts[(int64_t)k * c + ch];
-  out[ch] = accumulate ? out[ch] + s : s;
+static inline void cs_reduce(const float* parts, int nparts, int c, float* out, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((c + 63) / 64), dim3(256), 0, s, parts, nparts, c, out,
+                     accumulate);
 }
 
 // ---------------------------------------------------------------------------- elementwise
@@ -917,14 +943,13 @@ extern "C" int lic_channel_sum(int32_t dtype, const void* x, int32_t ldx, int32_
   const int threads = std::min(256, (c + 63) / 64 * 64);
   if (npix > 0) {
     TR_DISPATCH(dtype, "channel_sum",
-                hipLaunchKernelGGL(channel_sum_partial_kernel<T>, dim3(nparts), dim3(threads), 0, s, (const T*)x, ldx,
-                                   npix, c, per, ws));
+                hipLaunchKernelGGL(channel_sum_partial_kernel<T>, dim3(nparts, (c + 63) / 64), dim3(256), 0, s,
+                                   (const T*)x, ldx, npix, c, per, ws));
     LIC_CHECK_LAUNCH();
   } else {
     (void)hipMemsetAsync(ws, 0, (size_t)c * sizeof(float), s);
   }
-  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((c + 255) / 256), dim3(256), 0, s, ws, npix > 0 ? nparts : 1, c,
-                     out, accumulate);
+  cs_reduce(ws, npix > 0 ? nparts : 1, c, out, accumulate, s);
   LIC_CHECK_LAUNCH();
   return 0;
 }
@@ -1036,7 +1061,7 @@ extern "C" int lic_win_attn_bwd(const lic_attn_args* ap, const void* dout, int32
 }
 
 extern "C" int64_t lic_layernorm_bwd_workspace(int32_t npix, int32_t c) {
-  const int blocks = std::max(1, std::min(1024, (npix + 3) / 4));
+  const int blocks = std::max(1, std::min(256, (npix + 3) / 4));
   return (int64_t)blocks * 2 * c * (int64_t)sizeof(float);
 }
 
@@ -1045,7 +1070,7 @@ extern "C" int lic_layernorm_bwd(int32_t dtype, const void* x, int32_t ldx, cons
                                  float* dwb, int32_t accumulate, float* ws, int64_t ws_bytes, lic_stream_t stream) {
   if (npix <= 0 || c <= 0) return 0;
   if (c > 64 * 12) return fail("layernorm_bwd: C > 768");
-  const int blocks = std::max(1, std::min(1024, (npix + 3) / 4));
+  const int blocks = std::max(1, std::min(256, (npix + 3) / 4));
   if (ws_bytes < lic_layernorm_bwd_workspace(npix, c)) return fail("layernorm_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const int cpl = (c + 63) / 64;
@@ -1059,8 +1084,7 @@ extern "C" int lic_layernorm_bwd(int32_t dtype, const void* x, int32_t ldx, cons
   else LNB(12);
 #undef LNB
   LIC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((2 * c + 255) / 256), dim3(256), 0, s, ws, blocks, 2 * c, dwb,
-                     accumulate);
+  cs_reduce(ws, blocks, 2 * c, dwb, accumulate, s);
   LIC_CHECK_LAUNCH();
   return 0;
 }
@@ -1200,8 +1224,7 @@ extern "C" int lic_dwconv_wgrad(int32_t dtype, const void* x, int32_t ldx, const
               hipLaunchKernelGGL(dw_wgrad_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ldx, (const T*)dz, ldz, n, h,
                                  w, ho, wo, c, stride, ntaps, tp, per, ws));
   LIC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((ntaps * c + 255) / 256), dim3(256), 0, s, ws, nsplit,
-                     ntaps * c, dw, 0);
+  cs_reduce(ws, nsplit, ntaps * c, dw, 0, s);
   LIC_CHECK_LAUNCH();
   return 0;
 }
