@@ -224,6 +224,8 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
   }
   if (!active) return;
   // lane (query i, half h) holds channels c = 8g + 4h + (0..3), g = 0..3
+  // d % 8 == 0, so a lane's 4 channels are all in range or all out; with an aligned
+  // output (checked at dispatch) they go out as one 8-B (fp16) / 16-B (fp32) store
   T* out = (T*)a.out;
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti) {
@@ -233,9 +235,15 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
     for (int g = 0; g < 4; ++g) {
       const int c0 = 8 * g + 4 * lh;
       if (c0 >= d) continue;
+      if constexpr (sizeof(T) == 2) {
+        uint2 pk;
+        half_t* e = (half_t*)&pk;
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (c0 + e < d) op[c0 + e] = from_f<T>(O[ti][4 * g + e]);
+        for (int k = 0; k < 4; ++k) e[k] = (half_t)O[ti][4 * g + k];
+        *(uint2*)(op + c0) = pk;
+      } else {
+        *(float4*)(op + c0) = make_float4(O[ti][4 * g], O[ti][4 * g + 1], O[ti][4 * g + 2], O[ti][4 * g + 3]);
+      }
     }
   }
 }
@@ -243,7 +251,7 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
 int win_attn_mfma_dispatch(const lic_attn_args& a, hipStream_t s, int& status) {
   const int d = a.c / a.heads;
   if (a.ws != 8 || d > 32 || d % 8 || a.ldqkv % 8 || a.force_valu) return 0;
-  if ((uintptr_t)a.qkv % 16) return 0;
+  if ((uintptr_t)a.qkv % 16 || (uintptr_t)a.out % 16 || a.ldo % 4) return 0;
   const int64_t blocks = (int64_t)a.n * (a.h / 8) * (a.w / 8) * ((a.heads + 3) / 4);
   if (a.dtype == LIC_F16)
     hipLaunchKernelGGL(win_attn_mfma_kernel<half_t>, dim3((unsigned)blocks), dim3(256), 0, s, a);
