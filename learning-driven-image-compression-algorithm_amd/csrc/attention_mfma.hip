@@ -57,6 +57,22 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
   const T* qkv = (const T*)a.qkv;
   const int64_t ldq = a.ldqkv;
   const int qoff = hc * d, koff = a.c + hc * d, voff = 2 * a.c + hc * d;
+  // fp16: K/Q fragments straight from the qkv map (lane (row, h) holds channels
+  // 16s + 8h .. +7), issued before the V^T staging so all reads are in flight at once
+  half8 kf[2][2] = {}, qf[2][2] = {};
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = 16 * s + 8 * lh;
+      if (ch >= d) continue;
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const T* tp = qkv + (int64_t)pixs[32 * t2 + lr] * ldq;
+        kf[s][t2] = *(const half8*)(tp + koff + ch);
+        qf[s][t2] = *(const half8*)(tp + qoff + ch);
+      }
+    }
+  }
   // V^T staging: lane t loads its V row with 16-byte loads (d % (16 / sizeof(T)) == 0)
   // and scatters it transposed into vT[c][t] (zeros for c >= d)
   {
@@ -86,24 +102,14 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
       for (int r = 0; r < 16; ++r) S[x][y][r] = 0.f;
 
   if constexpr (sizeof(T) == 2) {
-    // fragments straight from the qkv map: lane (row, h) holds channels 16s + 8h .. +7
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int ch = 16 * s + 8 * lh;
       if (16 * s >= d) break;
-      half8 kf[2], qf[2];
-#pragma unroll
-      for (int t2 = 0; t2 < 2; ++t2) {
-        const int tok = 32 * t2 + lr;
-        half8 z = {};
-        kf[t2] = ch < d ? *(const half8*)(qkv + (int64_t)pixs[tok] * ldq + koff + ch) : z;
-        qf[t2] = ch < d ? *(const half8*)(qkv + (int64_t)pixs[tok] * ldq + qoff + ch) : z;
-      }
 #pragma unroll
       for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
-          S[tj][ti] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[tj], qf[ti], S[tj][ti], 0, 0, 0);
+          S[tj][ti] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s][tj], qf[s][ti], S[tj][ti], 0, 0, 0);
     }
   } else {
     for (int k = 0; k < d; k += 2) {
