@@ -1,6 +1,6 @@
 // Window attention on MFMA for 8x8 windows (64 tokens) and head_dim <= 32 (gfx950).
 //
-// One wave per (image, window, head); a workgroup holds 4 heads of one window.
+// One wave per (image, window, head); a workgroup holds 4 or 8 heads of one window.
 // Scores are computed transposed, S^T = K Q^T (keys on the accumulator rows,
 // queries on the lanes), so the softmax over keys of a query is a reduction over
 // the lane's own registers plus one exchange with lane^32, and the probability
@@ -20,14 +20,14 @@ namespace lic {
 constexpr int AT_N = 64;   // tokens per window (ws = 8)
 constexpr int VT_LD = 68;  // padded row (elements) of the V^T staging image
 
-template <typename T>
-__global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args a) {
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_args a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lr = lane & 31, lh = lane >> 5;
   const int d = a.c / a.heads;
   constexpr int ws = 8;
   const int nwx = a.w / ws, nwy = a.h / ws;
-  const int hgroups = (a.heads + 3) / 4;
+  const int hgroups = (a.heads + NW - 1) / NW;
   int bid = blockIdx.x;
   const int hg = bid % hgroups;
   bid /= hgroups;
@@ -35,12 +35,12 @@ __global__ __launch_bounds__(256) void win_attn_mfma_kernel(const lic_attn_args 
   bid /= nwx;
   const int wy = bid % nwy;
   const int b = bid / nwy;
-  const int h = hg * 4 + wave;
+  const int h = hg * NW + wave;
   const bool active = h < a.heads;
   const int hc = active ? h : 0;
 
-  __shared__ __attribute__((aligned(16))) T vT[4][32 * VT_LD];
-  __shared__ float tab[4][(2 * ws - 1) * (2 * ws - 1)];
+  __shared__ __attribute__((aligned(16))) T vT[NW][32 * VT_LD];
+  __shared__ float tab[NW][(2 * ws - 1) * (2 * ws - 1)];
   __shared__ int pixs[AT_N];
 
   // token t -> original pixel (roll(-shift) + window_partition as addressing)
@@ -258,11 +258,18 @@ int win_attn_mfma_dispatch(const lic_attn_args& a, hipStream_t s, int& status) {
   const int d = a.c / a.heads;
   if (a.ws != 8 || d > 32 || d % 8 || a.ldqkv % 8 || a.force_valu) return 0;
   if ((uintptr_t)a.qkv % 16 || (uintptr_t)a.out % 16 || a.ldo % 4) return 0;
-  const int64_t blocks = (int64_t)a.n * (a.h / 8) * (a.w / 8) * ((a.heads + 3) / 4);
-  if (a.dtype == LIC_F16)
-    hipLaunchKernelGGL(win_attn_mfma_kernel<half_t>, dim3((unsigned)blocks), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL(win_attn_mfma_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  // fp16 with 8+ heads on a big map: 8 waves (all heads of a window in one workgroup,
+  // one L2; 64x64 WBA 97 -> 77 us).  Small maps keep 4 waves for more workgroups, fp32
+  // for the LDS (its V^T image is twice the size)
+  const int64_t windows = (int64_t)a.n * (a.h / 8) * (a.w / 8);
+  const int nw = (a.dtype == LIC_F16 && a.heads >= 8 && windows >= 1024) ? 8 : 4;
+  const int64_t blocks = windows * ((a.heads + nw - 1) / nw);
+  if (a.dtype == LIC_F16) {
+    if (nw == 8) hipLaunchKernelGGL((win_attn_mfma_kernel<half_t, 8>), dim3((unsigned)blocks), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((win_attn_mfma_kernel<half_t, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((win_attn_mfma_kernel<float, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  }
   hipError_t e = hipGetLastError();
   status = e == hipSuccess ? 0 : fail(std::string("attn mfma launch: ") + hipGetErrorString(e));
   return 1;

@@ -100,3 +100,17 @@ def test_mfma_attention_strided_views(dtype):
     tol = 1e-4 if dtype == torch.float32 else 1e-2 * ref.abs().max().item()
     assert (got - ref).abs().max().item() <= tol
     assert out_buf[..., :16].eq(7).all() and out_buf[..., 16 + C:].eq(7).all()
+
+
+@pytest.mark.parametrize("C,heads,shift,mask_kind", [(192, 8, 4, 1), (288, 12, 0, 0)])
+def test_mfma_attention_8_wave_groups(C, heads, shift, mask_kind):
+    """fp16 on >= 1024 windows takes the 8-heads-per-workgroup launch (12 heads: a
+    second group with 4 idle waves)."""
+    ws, B, H, W = 8, 16, 64, 64
+    g = torch.Generator().manual_seed(C + heads)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g) * 0.5
+    scale = (C // heads) ** -0.5
+    ref = _attn_ref(qkv.to(torch.float16).float(), C, heads, ws, shift, table, mask_kind, False, scale)
+    out = _run(qkv, C, heads, ws, shift, table, mask_kind, False, scale, torch.float16, False)
+    assert (out - ref).abs().max().item() <= 1e-2 * (ref.abs().max().item() + 1e-6)
