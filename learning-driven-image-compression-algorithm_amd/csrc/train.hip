@@ -282,24 +282,36 @@ __global__ __launch_bounds__(256) void channel_sum_partial_kernel(const T* __res
   if (r == 0 && ch < c) parts[(int64_t)blockIdx.x * c + ch] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
-__global__ __launch_bounds__(256) void channel_sum_reduce_kernel(const float* __restrict__ parts, int nparts, int c,
-                                                                 float* __restrict__ out, int accumulate) {
-  __shared__ float red[4][64];
+// 64 channels x 16 part groups per 1024-thread block, 4 independent loads in flight per
+// thread: the serial chain per thread is nparts/64 adds (was nparts/4 dependent loads)
+__global__ __launch_bounds__(1024) void channel_sum_reduce_kernel(const float* __restrict__ parts, int nparts, int c,
+                                                                  float* __restrict__ out, int accumulate) {
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, r = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (ch < c)
-    for (int k = r; k < nparts; k += 4) s += parts[(int64_t)k * c + ch];
-  red[r][lane] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (ch < c) {
+    int k = r;
+    for (; k + 48 < nparts; k += 64) {
+      s0 += parts[(int64_t)k * c + ch];
+      s1 += parts[(int64_t)(k + 16) * c + ch];
+      s2 += parts[(int64_t)(k + 32) * c + ch];
+      s3 += parts[(int64_t)(k + 48) * c + ch];
+    }
+    for (; k < nparts; k += 16) s0 += parts[(int64_t)k * c + ch];
+  }
+  red[r][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (r == 0 && ch < c) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += red[g][lane];
     out[ch] = accumulate ? out[ch] + t : t;
   }
 }
 
 static inline void cs_reduce(const float* parts, int nparts, int c, float* out, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((c + 63) / 64), dim3(256), 0, s, parts, nparts, c, out,
+  hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((c + 63) / 64), dim3(1024), 0, s, parts, nparts, c, out,
                      accumulate);
 }
 
