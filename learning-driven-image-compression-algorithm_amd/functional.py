@@ -171,8 +171,15 @@ def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
     epc = 8 if dtype == torch.float16 else 4
     cpad = _cpad_for(cin, dtype) if (groups == 1 and cin % epc == 0) else cin
     copad = _choose_copad(co)
-    w = torch.zeros((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
-    w[:co, :, :cig] = weight.detach().permute(0, 2, 3, 1).reshape(co, kh * kw, cig).to(dtype)
+    # one permute+cast copy kernel (plus a fill when padded): the training path re-packs
+    # every conv each step, so launches count
+    src = weight.detach().permute(0, 2, 3, 1).reshape(co, kh * kw, cig)
+    if copad == co and cpad == cig:
+        w = torch.empty((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
+        w.copy_(src)
+    else:
+        w = torch.zeros((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
+        w[:co, :, :cig].copy_(src)
     dy = [ky - pt for ky in range(kh) for kx in range(kw)]
     dx = [kx - pl for ky in range(kh) for kx in range(kw)]
     b = bias.detach().float().contiguous() if bias is not None else None
