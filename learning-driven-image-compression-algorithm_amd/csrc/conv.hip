@@ -45,10 +45,6 @@ static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status
     if (a.copad % 64 == 0 && blocks(16, 16, 64) >= 200) return try_halo<T, 16, 16, 64, 4, 2>(a, s, status);
     if (a.copad % 32 == 0 && blocks(16, 16, 32) >= 200) return try_halo<T, 16, 16, 32, 8, 1>(a, s, status);
   }
-  // 16x8 tiles halve the weight bytes streamed per FLOP; taken where the 8x8 grid
-  // would run 1.5 or more blocks per CU (slice-loop 192-channel convs: +0.8 % end
-  // to end; an 8x8 x 32-channel grid for the 64-channel convs measured +-0)
-  if (a.mi > 8 && a.copad % 64 == 0 && blocks(16, 8, 64) >= 192) return try_halo<T, 16, 8, 64, 2, 2>(a, s, status);
   if (a.copad % 64 == 0 && blocks(8, 8, 64) >= 128) return try_halo<T, 8, 8, 64, 2, 2>(a, s, status);
   if (a.copad % 32 == 0 && blocks(8, 8, 32) >= 64) return try_halo<T, 8, 8, 32, 2, 1>(a, s, status);
   return 0;

@@ -1,5 +1,5 @@
 """GPU parity of the narrow / small-map halo conv configurations (BN 64 / 32,
-8x8- and 16x8-pixel tiles) that the slice loop's 16x16 latents and the 16-channel output
+8x8-pixel tiles) that the slice loop's 16x16 latents and the 16-channel output
 ConvTranspose take, against the generic implicit-GEMM kernel and fp32 torch CPU."""
 import pytest
 import torch
@@ -28,9 +28,6 @@ def _close(out, ref, dtype, tol32=1e-4):
     (64, 64, 7, 1, (3, 3, 3, 3), 16, 16),     # 49 taps (tap groups) on 8x8 tiles
     (96, 96, 3, 1, (1, 1, 1, 1), 16, 50),     # BN 32, ragged 16x16 tiles
     (192, 64, 3, 1, (1, 1, 1, 1), 16, 64),    # BN 64, 16x16 tiles
-    (320, 256, 3, 1, (1, 1, 1, 1), 32, 16),   # 16x8 tiles (8x8 grid: 2 blocks per CU)
-    (256, 256, 3, 1, (1, 1, 1, 1), 32, 12),   # 16x8 tiles, ragged in both directions
-    (192, 256, 5, 1, (2, 2, 2, 2), 32, 16),   # 16x8 tiles, 25 taps
 ])
 def test_small_halo_matches_generic_and_cpu(dtype, cin, cout, k, s, pad, B, H):
     from lic_amd.layers import Conv2d
@@ -63,15 +60,13 @@ def test_convT_to_16_channels(dtype, B, H):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("C", [64, 256])
-def test_small_halo_fused_epilogues(dtype, C):
-    """Residual, gate and GDN epilogues through the 8x8-tile (C=64) and 16x8-tile
-    (C=256) configs."""
+def test_small_halo_fused_epilogues(dtype):
+    """Residual, gate and GDN epilogues through the 8x8-tile config."""
     from lic_amd.layers import Conv2d
     import lic_amd.functional as Fn
     from lic_amd._ffi import EPI_GATE, EPI_GDN_DIV, ACT_GELU
     torch.manual_seed(32)
-    B, H = 32, 16
+    B, C, H = 32, 64, 16
     m = Conv2d(C, C, 3, 1, 1).to(DEV)
     xc = torch.randn(B, C, H, H)
     rc, gc, r2c = torch.randn(B, C, H, H), torch.randn(B, C, H, H), torch.randn(B, C, H, H)
