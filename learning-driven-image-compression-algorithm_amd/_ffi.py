@@ -225,7 +225,13 @@ def load():
     return lib
 
 
+_SYNC_EACH = os.environ.get("LIC_SYNC_EACH", "") not in ("", "0")   # debugging aid: device sync per call
+
+
 def check(status: int):
+    if _SYNC_EACH:
+        import torch
+        torch.cuda.synchronize()
     if status != 0:
         msg = _lib.lic_last_error().decode() if _lib is not None else "unknown"
         raise LicError(msg)

@@ -39,20 +39,21 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
   const bool active = h < a.heads;
   const int hc = active ? h : 0;
 
+  // Every LDS image is private to its wave (no cross-wave data: only wave-local
+  // ordering is needed, see wave_lds_sync).
   __shared__ __attribute__((aligned(16))) T vT[NW][32 * VT_LD];
   __shared__ float tab[NW][(2 * ws - 1) * (2 * ws - 1)];
-  __shared__ int pixs[AT_N];
 
-  // token t -> original pixel (roll(-shift) + window_partition as addressing)
-  if (threadIdx.x < AT_N) {
-    const int t = threadIdx.x;
+  // token t -> original pixel (roll(-shift) + window_partition as addressing),
+  // computed in registers by each lane that needs it
+  auto pix_of = [&](int t) -> int {
     int py = wy * ws + t / ws + a.shift, px = wx * ws + t % ws + a.shift;
     if (py >= a.h) py -= a.h;
     if (px >= a.w) px -= a.w;
-    pixs[t] = (b * a.h + py) * a.w + px;
-  }
+    return (b * a.h + py) * a.w + px;
+  };
+  const int pix_lr0 = pix_of(lr), pix_lr1 = pix_of(32 + lr);
   for (int k = lane; k < (2 * ws - 1) * (2 * ws - 1); k += 64) tab[wave][k] = a.table[k * a.tab_sr + hc * a.tab_sh];
-  __syncthreads();
 
   const T* qkv = (const T*)a.qkv;
   const int64_t ldq = a.ldqkv;
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
       if (ch >= d) continue;
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
-        const T* tp = qkv + (int64_t)pixs[32 * t2 + lr] * ldq;
+        const T* tp = qkv + (int64_t)(t2 ? pix_lr1 : pix_lr0) * ldq;
         kf[s][t2] = *(const half8*)(tp + koff + ch);
         qf[s][t2] = *(const half8*)(tp + qoff + ch);
       }
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
   // and scatters it transposed into vT[c][t] (zeros for c >= d)
   {
     constexpr int VE = 16 / (int)sizeof(T);
-    const T* vp = qkv + (int64_t)pixs[lane] * ldq + voff;
+    const T* vp = qkv + (int64_t)pix_of(lane) * ldq + voff;
 #pragma unroll
     for (int c0 = 0; c0 < 32; c0 += VE) {
       u32x4 raw = {0u, 0u, 0u, 0u};
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
       for (int k = 0; k < VE; ++k) vT[wave][(c0 + k) * VT_LD + lane] = e[k];
     }
   }
-  __syncthreads();
+  wave_lds_sync();  // the wave's tab / V^T writes before its reads (wave-private images)
 
   // fp32 keeps the reference's order (q*scale before the dot unless scale_after);
   // fp16 operands stay unscaled and the scale is applied to the fp32 dot
@@ -117,9 +118,9 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
       float kf[2], qf[2];
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
-        const int tok = 32 * t2 + lr;
-        kf[t2] = ch < d ? to_f(qkv[(int64_t)pixs[tok] * ldq + koff + ch]) : 0.f;
-        qf[t2] = ch < d ? to_f(qkv[(int64_t)pixs[tok] * ldq + qoff + ch]) * pre : 0.f;
+        const int64_t pt = t2 ? pix_lr1 : pix_lr0;
+        kf[t2] = ch < d ? to_f(qkv[pt * ldq + koff + ch]) : 0.f;
+        qf[t2] = ch < d ? to_f(qkv[pt * ldq + qoff + ch]) * pre : 0.f;
       }
 #pragma unroll
       for (int tj = 0; tj < 2; ++tj)
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti) {
     const int i = 32 * ti + lr;
-    T* op = out + (int64_t)pixs[i] * a.ldo + h * d;
+    T* op = out + (int64_t)(ti ? pix_lr1 : pix_lr0) * a.ldo + h * d;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c0 = 8 * g + 4 * lh;

@@ -403,6 +403,7 @@ class Net(nn.Module):
             self.add_mean = MeanShift(1.0, (0.4488, 0.4371, 0.4040), (1.0, 1.0, 1.0), 1)
             self.add_mean.apply(weight_init)
         self.last: Dict[str, torch.Tensor] = {}
+        self.last_coder: Dict[str, torch.Tensor] = {}   # views of compress()/decompress() buffers
 
     # ---- hyper prior (overridden by net_unet_ha_hs)
     _eb_channels = 192
@@ -447,6 +448,8 @@ class Net(nn.Module):
 
     def _side_stream(self, device, k: int = 0):
         """Per-device side streams for the independent branches of the graph."""
+        if self.__dict__.get("_lic_single_stream"):
+            return torch.cuda.current_stream(device)
         ss = self.__dict__.setdefault("_lic_streams", {})
         key = (str(device), k)
         if key not in ss:
@@ -595,6 +598,7 @@ class Net(nn.Module):
         ywords, yoff = EC.encode_streams(Act(SYM), Act(IDX), cs["gauss"])
         # the rounded syntax vector (net_ga.py:1016) travels as M int32 side values per image
         syntax = syn_r.nchw().reshape(B, self.M).float().to(torch.int32)
+        self.last_coder = dict(means=MU.t, scales=SC.t, indexes=IDX, z_hat=z_hat.t, y_hat=MS.t[..., 192:])
         return {"strings": [EC.to_strings(ywords, yoff, B, 192), EC.to_strings(zwords, zoff, B, z.c)],
                 "shape": (z.H, z.W), "syntax": syntax.cpu(), "symbols": SYM}
 
@@ -633,6 +637,7 @@ class Net(nn.Module):
         self._slice_loop(None, MS, SS, LR, MU, SC, SYM, None, partials, nper, decode=dec)
         if int(status[:B * zc].sum()) or int(ystat.sum()):
             raise ValueError("decompress: corrupt bitstream")
+        self.last_coder = dict(means=MU.t, scales=SC.t, z_hat=z_hat.t, y_hat=MS.t[..., 192:])
         x_tilde = self.s_model.run(MS.ch(192, 384))
         syn = Act(syntax.to(dev).to(dt).reshape(B, 1, 1, self.M).contiguous())
         cw = self.conv_weights_gen.run(syn)
