@@ -23,6 +23,8 @@ import math
 from typing import Dict, List, Optional
 
 import numpy as np
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -429,7 +431,7 @@ class Net(nn.Module):
     def _hyper_s(self, z_hat: Act, means_out: Act, scales_out: Act):
         """latent_means / latent_scales from z_hat (the decoder side of :1004-1007)."""
         main = torch.cuda.current_stream(z_hat.t.device)
-        side = self._side_stream(z_hat.t.device, 1)
+        side = self._side_stream(z_hat.t.device, 1, "hyper")
         side.wait_stream(main)
         with torch.cuda.stream(side):
             _run_seq_gelu(self.h_scale_s, z_hat, scales_out)
@@ -446,9 +448,9 @@ class Net(nn.Module):
             self.__dict__["_med_cache"] = c
         return c[1]
 
-    def _side_stream(self, device, k: int = 0):
+    def _side_stream(self, device, k: int = 0, part: str = ""):
         """Per-device side streams for the independent branches of the graph."""
-        if self.__dict__.get("_lic_single_stream"):
+        if self.__dict__.get("_lic_single_stream") or (part and part in os.environ.get("LIC_DEBUG_SERIAL", "")):
             return torch.cuda.current_stream(device)
         ss = self.__dict__.setdefault("_lic_streams", {})
         key = (str(device), k)
@@ -509,7 +511,7 @@ class Net(nn.Module):
         dev = MS.t.device
         ns, sw = self.num_slices, 192 // self.num_slices
         main = torch.cuda.current_stream(dev)
-        side2 = self._side_stream(dev, 1)
+        side2 = self._side_stream(dev, 1, "slice")
         for i in range(ns):
             ci = 192 + sw * min(i, 4)
             # the scale branch (:1042-1046) is independent of the mean branch (:1034-1040)
@@ -657,7 +659,7 @@ class Net(nn.Module):
         z3 = self.a_model.run(x)                                  # net_ga.py:988
         hh, ww = z3.H, z3.W
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev)
+        side = self._side_stream(dev, 0, "syntax")
         # syntax head (net_ga.py:1010-1016, :1083) only meets the main chain at the
         # reconstruction: it runs concurrently on a side stream (joined below)
         side.wait_stream(main)

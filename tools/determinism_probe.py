@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--no-poison", action="store_true")
     ap.add_argument("--poison-random", action="store_true", help="fill freed blocks with random finite fp16")
     ap.add_argument("--single-stream", action="store_true", help="run the side-stream branches on the current stream")
+    ap.add_argument("--forward-only", action="store_true")
     args = ap.parse_args()
     from lic_amd.model import net_ga
     torch.manual_seed(0)
@@ -99,6 +100,12 @@ def main():
         pz()
         fw.append(diff(ref, fwd(), {"means": 1, "scales": 1, "y_hat": 1, "symbols": 1}))
     report["forward_diffs"] = fw
+    report["serial_parts"] = os.environ.get("LIC_DEBUG_SERIAL", "")
+    if args.forward_only:
+        report["ok"] = all(not d for d in fw)
+        report["n_bad"] = sum(1 for d in fw if d)
+        print(json.dumps(report), flush=True)
+        sys.exit(0 if report["ok"] else 1)
 
     net.update()
     enc = net.compress(x)

@@ -15,6 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 TRACE = []
+PRE = [None]   # optional hook run before every wrapped launch (LDS poisoning)
 
 
 def _h(a):
@@ -33,6 +34,21 @@ def _h(a):
 def install():
     from lic_amd import functional as Fn
     orig_conv = Fn.conv
+    lib = Fn._lib()
+
+    class _Proxy:   # PRE hook before every liblic launch
+        def __getattr__(self, name):
+            f = getattr(lib, name)
+            if not name.startswith("lic_") or name.endswith(("_workspace", "_parts")) or name == "lic_last_error":
+                return f
+
+            def call(*a):
+                if PRE[0]:
+                    PRE[0]()
+                return f(*a)
+            return call
+    proxy = _Proxy()
+    Fn._lib = lambda: proxy
 
     def conv(x, pk, out=None, **kw):
         y = orig_conv(x, pk, out, **kw)
@@ -67,6 +83,11 @@ def main():
     ap.add_argument("--precision", default="fp16")
     ap.add_argument("--what", default="forward", choices=["forward", "a_model", "a_model_layers"])
     ap.add_argument("--poison-random", action="store_true")
+    ap.add_argument("--multi-stream", action="store_true", help="keep the side streams (default: single stream)")
+    ap.add_argument("--lds-poison", action="store_true", help="fill every CU's LDS with a new pattern before each run")
+    ap.add_argument("--lds-poison-each", action="store_true",
+                    help="fill every CU's LDS with the run's pattern before every launch (finds kernels that read "
+                         "LDS they did not write: the first differing launch is the culprit)")
     args = ap.parse_args()
     if args.what != "a_model_layers":
         install()
@@ -75,7 +96,8 @@ def main():
     torch.manual_seed(0)
     B = args.batch
     net = net_ga.Net((B, 256, 256, 3), (B, 256, 256, 3), False, False, precision=args.precision).to("cuda")
-    net.__dict__["_lic_single_stream"] = True
+    if not args.multi_stream:
+        net.__dict__["_lic_single_stream"] = True
     x = (torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1)) * 2 - 1).to("cuda")
 
     layers = []
@@ -92,9 +114,19 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from determinism_probe import poison
 
+    from lds_poison import poison_lds
+    nrun = [0]
+
+    if args.lds_poison_each:
+        PRE[0] = lambda: poison_lds(nrun[0])
+
     def once():
+        nrun[0] += 0 if args.lds_poison else 1
         if args.poison_random:
             poison(random=True)
+        if args.lds_poison:
+            nrun[0] += 1
+            poison_lds(nrun[0])
         if args.what == "a_model_layers":
             layers.clear()
             net.a_model.run(Act.from_nchw(x, net.dtype, pad16=True))
