@@ -106,6 +106,8 @@ def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=Fals
                 wp = weight_path.format(lmbda=lmbda) if weight_path else ""
                 if wp and os.path.exists(wp):
                     net.load_state_dict(torch.load(wp, map_location="cpu", weights_only=True), strict=True)
+                else:
+                    net_ga.synthetic_syntax_bias_(net, li)
                 xin = torch.empty_like(x)
                 nets[key] = (net, xin)
                 if graph:
@@ -197,6 +199,7 @@ def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing,
             net.load_state_dict(torch.load(weight_path, map_location="cpu", weights_only=True), strict=True)
         else:
             print(f"warning: checkpoint {weight_path!r} not found; using the seeded reference initialisation")
+            net_ga.synthetic_syntax_bias_(net)
         torch.cuda.synchronize()
         begin_time = time.time()
         if pre_processing:

@@ -226,6 +226,25 @@ class synthesisTransformModel(nn.Module):
         return self.run(Act.from_nchw(inputs)).nchw()
 
 
+def synthetic_syntax_bias_(net: nn.Module, seed: int = 0) -> nn.Module:
+    """Synthetic-weights helper (no checkpoints exist for any lambda).
+
+    With the reference's init (weight_init zeroes every conv bias, net_ga.py:723-729) the
+    Syntax_Model output of a seeded net stays inside (-0.5, 0.5), so round(syntax) = 0,
+    conv_weights_gen maps it to all-zero 1x1 weights and x_rec = tanh(0) everywhere: the
+    reconstruction and PSNR would not depend on s_model at all.  This offsets the 16 biases of
+    Syntax_Model.conv by k + 0.1 (k seeded in {-2..2}), so the rounded syntax is non-zero, the
+    generated per-image weights are non-zero and x_rec = tanh(batch_conv(w, x_tilde)) carries
+    the decoder's output.  Used for every synthetic-weights run (golden fixtures, GPU parity
+    tests, bench, eval_net's synthetic sweep); the CPU oracle reads the same state_dict."""
+    g = torch.Generator().manual_seed(1000 + seed)
+    b = net.syntax_model.conv.bias
+    k = torch.randint(-2, 3, (b.numel(),), generator=g).float() + 0.1
+    with torch.no_grad():
+        b.copy_(k.to(b.device, b.dtype))
+    return net
+
+
 def _run_seq_gelu(seq: nn.Sequential, x: Act, out: Optional[Act] = None) -> Act:
     """conv (GELU conv)* stacks of net_ga.py:811-845; subpel convs fuse PixelShuffle(2)."""
     mods = list(seq)
@@ -678,10 +697,13 @@ class Net(nn.Module):
         main.wait_stream(side)                                     # syntax head joined
         self._reconstruct(x_tilde, syn_r, cw, x_in, x_rec, sq_parts, ppi)
         if return_intermediates:
+            # the syntax vector before bypass_round (net_ga.py:1010-1016; one extra small pass
+            # on this debug path only) next to the rounded one the generator consumed
+            syn_raw = self.syntax_model.run(z3.ch(0, self.M), rounded=False)
             self.last = dict(z3=z3.nchw(), z=z.nchw(), z_hat=z_hat.nchw(), latent_means=MS.ch(0, 192).nchw(),
                              latent_scales=SS.ch(0, 192).nchw(), y_hat=y_hat.nchw(), means=MU.nchw(),
                              scales=SC.nchw(), symbols=SYM.permute(0, 3, 1, 2), likelihoods=LIK.permute(0, 3, 1, 2),
-                             x_tilde=x_tilde.nchw(), x_rec=x_rec, syntax=syn_r.nchw())
+                             x_tilde=x_tilde.nchw(), x_rec=x_rec, syntax=syn_raw.nchw(), syntax_r=syn_r.nchw())
 
     def _reconstruct(self, x_tilde: Act, syn_r: Act, cw: Act, x_in: Optional[torch.Tensor], x_rec: torch.Tensor,
                      sq_parts: Optional[torch.Tensor], ppi: int):

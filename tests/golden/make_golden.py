@@ -17,8 +17,12 @@ Files (numpy .npz, no pickles):
   net_unet_ha_hs_256.npz  same for model/net_unet_ha_hs.py.
   source_net_256.npz      source_net z (BASELINE config 1), 1x3x256x256.
 Network weights are not stored (67 M parameters): they are re-created by
-torch.manual_seed(seed) + the reference's init (weight_init, net_ga.py:723-729);
+torch.manual_seed(seed) + the reference's init (weight_init, net_ga.py:723-729) +
+lic_amd.model.net_ga.synthetic_syntax_bias_ (Syntax_Model.conv bias offset so that the
+rounded syntax and hence the reconstruction are not identically zero);
 `param_sum` / `param_abs_sum` pin that the regenerated weights are identical.
+The net fixtures hold the syntax vector before rounding, x_tilde (every 8th pixel),
+x_rec as uint8 (non-constant: asserted) and the per-slice symbols / bpp / PSNR.
 
 usage: python tests/golden/make_golden.py
 """
@@ -49,7 +53,15 @@ def make_net(arch, size=SIZE, seed=NET_SEED):
     from lic_amd.model import net_ga, net_unet_ha_hs, source_net
     torch.manual_seed(seed)
     mod = {"net_ga": net_ga, "net_unet_ha_hs": net_unet_ha_hs, "source_net": source_net}[arch]
-    return mod.Net((1, size, size, 3), (1, size, size, 3), False, False, precision="fp32")
+    net = mod.Net((1, size, size, 3), (1, size, size, 3), False, False, precision="fp32")
+    if arch != "source_net":
+        net_ga.synthetic_syntax_bias_(net, seed)
+    return net
+
+
+def x_rec_u8(x_rec):
+    """x_hat of net_ga.py:1137 as uint8."""
+    return torch.round(torch.clamp((x_rec + 1) * 127.5, 0, 255)).to(torch.uint8)
 
 
 def state_of(net):
@@ -129,10 +141,14 @@ def make_net_fixture(arch):
     r = R.net_forward(x, P, arch=arch)
     sym = r["symbols"]
     assert sym.abs().max() < 2 ** 15
-    np.savez(os.path.join(HERE, f"{arch}_{SIZE}.npz"), net_seed=NET_SEED, x_seed=X_SEED, size=SIZE,
-             param_sum=s, param_abs_sum=a, bpp=r["bpp"].numpy(), v_psnr=r["v_psnr"].numpy(),
-             v_mse=r["v_mse"].numpy(), symbols=sym.to(torch.int16).numpy(), z_hat=r["z_hat"].numpy(),
-             x_rec_u8=torch.round(torch.clamp((r["x_rec"] + 1) * 127.5, 0, 255)).to(torch.uint8).numpy())
+    u8 = x_rec_u8(r["x_rec"])
+    assert u8.unique().numel() > 1, "degenerate reconstruction (syntax rounds to 0)"
+    assert torch.round(r["syntax"]).abs().sum() > 0
+    np.savez_compressed(os.path.join(HERE, f"{arch}_{SIZE}.npz"), net_seed=NET_SEED, x_seed=X_SEED, size=SIZE,
+                        param_sum=s, param_abs_sum=a, bpp=r["bpp"].numpy(), v_psnr=r["v_psnr"].numpy(),
+                        v_mse=r["v_mse"].numpy(), symbols=sym.to(torch.int16).numpy(), z_hat=r["z_hat"].numpy(),
+                        syntax=r["syntax"].numpy(), x_tilde_s8=r["x_tilde"][:, :, ::8, ::8].contiguous().numpy(),
+                        x_rec_u8=u8.numpy())
 
 
 if __name__ == "__main__":

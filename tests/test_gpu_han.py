@@ -61,15 +61,18 @@ def test_net_post_processing_fp32_parity(arch):
     from lic_amd.model import net_ga, net_unet_ha_hs
     torch.manual_seed(0)
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
-    net = mod.Net((1, 256, 256, 3), (1, 256, 256, 3), False, True, precision="fp32")
+    net = net_ga.synthetic_syntax_bias_(mod.Net((1, 256, 256, 3), (1, 256, 256, 3), False, True, precision="fp32"))
     with torch.no_grad():
         net.HAN.la.gamma.fill_(0.25)
         net.HAN.csa.gamma.fill_(0.5)
     P = {k: v.detach().float().cpu() for k, v in net.state_dict().items()}
     net = net.to(DEV)
     x = torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(6)) * 2 - 1
-    bpp, v_mse, v_psnr = net(x.to(DEV), "test")
+    bpp, v_mse, v_psnr = net(x.to(DEV), "test", return_intermediates=True)
     ref = R.net_forward(x, P, arch=arch, post_processing=True)
+    u8 = lambda t: torch.round(torch.clamp((t.float().cpu() + 1) * 127.5, 0, 255)).int()
+    d8 = (u8(net.last["x_rec"]) - u8(ref["x_rec"])).abs()
+    assert u8(ref["x_rec"]).unique().numel() > 16 and int(d8.max()) <= 1 and (d8 > 0).float().mean() < 1e-4
     print(f"\n[{arch} +HAN fp32] bpp {bpp.item():.8f}/{ref['bpp'].item():.8f} "
           f"psnr {v_psnr.item():.6f}/{ref['v_psnr'].item():.6f}")
     assert abs(bpp.item() - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item()))

@@ -332,6 +332,10 @@ def test_loud_failure_on_bad_args():
     (96, 96, 3, 1, (1, 1, 1, 1), 16, 50),     # ragged tile edges, BN=128 pad
     (64, 64, 3, 1, (1, 1, 1, 1), 8, 256),     # HAN conv3x3 @ full res (fp16: 32x16 px x 64 ch tiles)
     (64, 64, 3, 1, (1, 1, 1, 1), 9, 250),     # same, ragged 32x16 tiles
+    # the bench's configuration (B=32 at 64x64 -> fp16 32x16-px x 192-ch tiles, conv.hip)
+    (192, 192, 3, 1, (1, 1, 1, 1), 32, 64),
+    (192, 192, 7, 1, (3, 3, 3, 3), 32, 64),
+    (192, 192, 3, 1, (1, 1, 1, 1), 28, 56),   # ragged 32x16 tiles (56 = 32 + 24, 56 = 3*16 + 8)
 ])
 def test_conv_halo_matches_generic(dtype, cin, cout, k, s, pad, B, H):
     """The spatial-tile (halo) kernel and the generic implicit-GEMM kernel agree."""
@@ -356,3 +360,27 @@ def test_conv_transpose_halo_matches_cpu(dtype):
     out = m.run(_act(x, dtype), prepad=(1, 1)).nchw()
     ref = F.conv_transpose2d(F.pad(x, (1, 0, 1, 0)), m.weight.cpu(), m.bias.cpu(), 2, 3, 1)
     _close(out, ref, dtype)
+
+
+def _big_tile_selected(B, H, co=192):
+    """Mirror of conv.hip's fp16 tile choice: 32x16 px x 192 ch when the grid has >= 200
+    such workgroups (stride 1, co % 192 == 0, map taller than 16)."""
+    return co % 192 == 0 and H > 16 and B * (-(-H // 32)) * (-(-H // 16)) * (co // 192) >= 200
+
+
+@pytest.mark.parametrize("k,B,H", [(3, 32, 64), (7, 32, 64), (3, 28, 56)])
+def test_conv_halo_32x16_tile_fp16_vs_torch_fp32(k, B, H):
+    """The headline kernel configuration (fp16 conv_halo_kernel<32,16,192>, the bench's
+    roofline kernel) against torch fp32 on the CPU: fp16 operands, fp32 accumulation."""
+    from lic_amd.layers import Conv2d
+    assert _big_tile_selected(B, H)
+    torch.manual_seed(17)
+    m = Conv2d(192, 192, k, 1, k // 2)
+    x = torch.randn(B, 192, H, H) * 0.5
+    out = m.to(DEV).run(_act(x, torch.float16)).nchw().float().cpu()
+    # reference on the fp16-rounded operands, so the bar measures the kernel, not the cast
+    ref = F.conv2d(x.half().float(), m.weight.detach().cpu().half().float(), m.bias.detach().cpu(), 1, k // 2)
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    print(f"\n[conv{k}x{k} fp16 32x16 tile B={B} {H}x{H}] max err {err:.3e} (scale {scale:.2f})")
+    assert err <= 4e-3 * scale

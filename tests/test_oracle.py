@@ -162,3 +162,22 @@ def test_han_lam_csam_identity_at_zero_gamma_and_lam_known_answer():
     out = R.han_lam(e0, torch.ones(1)).view(1, 2, 1, 1, 2)
     a_self, a_other = 1 / (1 + math.e), math.e / (1 + math.e)
     torch.testing.assert_close(out[0, 0, 0, 0], torch.tensor([1 + a_self, a_other]))
+
+
+def test_parity_check_symbols_accepts_only_near_ties():
+    """tests/parity.check_symbols: a flip at a near-.5 tie of the oracle's y - mu passes, a flip
+    anywhere else fails."""
+    import pytest as _pt
+    from parity import check_symbols
+    g = torch.Generator().manual_seed(0)
+    z3 = torch.randn(1, 8, 16, 16, generator=g) * 3
+    mu = torch.randn(1, 8, 16, 16, generator=g)
+    z3[0, 5, 3, 3] = mu[0, 5, 3, 3] + 2.5 + 1e-5           # near-tie
+    ref = {"z3": z3, "means": mu, "symbols": torch.round(z3 - mu).to(torch.int32)}
+    sym = ref["symbols"].clone()
+    assert check_symbols(sym, ref) == 0
+    sym[0, 5, 3, 3] += 1
+    assert check_symbols(sym, ref, max_rate=1e-2) == 1
+    sym[0, 1, 12, 12] += 1                                   # no tie, no earlier flip nearby
+    with _pt.raises(AssertionError):
+        check_symbols(sym, ref, max_rate=1e-2)
