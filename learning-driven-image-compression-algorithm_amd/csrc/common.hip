@@ -1,6 +1,9 @@
 // Error handling and library info for liblic.
 #include "lic_common.h"
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <tuple>
 
 namespace lic {
 static thread_local std::string g_err;
@@ -8,6 +11,20 @@ void set_error(const std::string& s) { g_err = s; }
 int fail(const std::string& s) {
   g_err = s;
   return 1;
+}
+
+hipError_t ensure_dyn_lds(const void* kern, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::set<std::tuple<const void*, int, int>> done;
+  const auto key = std::make_tuple(kern, dev, bytes);
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count(key)) return hipSuccess;
+  e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert(key);
+  return e;
 }
 }  // namespace lic
 

@@ -364,10 +364,10 @@ int try_halo(const lic_conv_args& a, hipStream_t s, int& status) {
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   dim3 grid((unsigned)blocks, a.copad / BN);
   auto kern = conv_halo_kernel<T, TH, TW, BN, WM, WN>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
+  const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
+  if (ea != hipSuccess) {
+    status = fail(std::string("halo conv: dynamic LDS attribute: ") + hipGetErrorString(ea));
+    return 1;
   }
   hipLaunchKernelGGL(kern, grid, dim3(NT), smem, s, a, p);
   hipError_t e = hipGetLastError();

@@ -17,6 +17,11 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 void set_error(const std::string& s);
 int fail(const std::string& s);
 
+// Raise `kern`'s dynamic-LDS limit to `bytes` on the current device, once per
+// (kernel, device, size); thread-safe, returns the HIP status of the first attempt
+// (a failure is not cached, so the next launch tries again).
+hipError_t ensure_dyn_lds(const void* kern, int bytes);
+
 #define LIC_CHECK_LAUNCH()                                                   \
   do {                                                                       \
     hipError_t _e = hipGetLastError();                                       \

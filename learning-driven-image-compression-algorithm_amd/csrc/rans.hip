@@ -534,6 +534,7 @@ extern "C" int32_t lic_rans_cap(int32_t hw) {
 }
 
 extern "C" int lic_rans_encode(const lic_rans_args* a, lic_stream_t stream) {
+  if (!a) return fail("rans_encode: null args");
   const int64_t ns = (int64_t)a->n * a->c;
   if (ns == 0) return 0;
   if (!a->symbols || !a->cdfs || !a->cdf_sizes || !a->offsets || !a->scratch || !a->lengths)
@@ -557,6 +558,7 @@ extern "C" int lic_rans_pack(const uint32_t* scratch, int32_t cap, const int32_t
 }
 
 extern "C" int lic_rans_decode(const lic_rans_args* a, lic_stream_t stream) {
+  if (!a) return fail("rans_decode: null args");
   const int64_t ns = (int64_t)a->n * a->c;
   if (ns == 0) return 0;
   if (!a->words || !a->offsets_w || !a->cdfs || !a->cdf_sizes || !a->offsets)
@@ -567,14 +569,9 @@ extern "C" int lic_rans_decode(const lic_rans_args* a, lic_stream_t stream) {
   const int64_t worst = (int64_t)a->ncdf * a->cdf_stride;
   const int lds_words = a->ncdf <= kDecMaxStagedTables ? (int)(worst < kDecLdsWords ? worst : kDecLdsWords) : 0;
   const size_t lds = (size_t)lds_words * sizeof(int32_t);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)rans_decode_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kDecLdsWords * 4);
-    (void)hipFuncSetAttribute((const void*)rans_decode_kernel<half_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kDecLdsWords * 4);
-    attr_set = true;
-  }
+  const void* kern = a->dtype == LIC_F32 ? (const void*)rans_decode_kernel<float> : (const void*)rans_decode_kernel<half_t>;
+  const hipError_t ea = ensure_dyn_lds(kern, kDecLdsWords * 4);
+  if (ea != hipSuccess) return fail(std::string("rans_decode: dynamic LDS attribute: ") + hipGetErrorString(ea));
   const dim3 grid((unsigned)((ns + 63) / 64));
   if (a->dtype == LIC_F32)
     hipLaunchKernelGGL(rans_decode_kernel<float>, grid, dim3(64), lds, s, *a, lds_words);
