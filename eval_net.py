@@ -172,7 +172,7 @@ def finetune_encoder(net, data, lmbda, tune_iter):
 
 
 def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing, tune_iter, arch="net_ga",
-        precision="fp32", all_images=False, device="cuda"):
+        precision="fp32", all_images=False, device="cuda", noise_seed=None):
     from lic_amd.model import net_ga, net_unet_ha_hs
     from lic_amd import distributed as D
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
@@ -205,7 +205,7 @@ def val(data_path, weight_path, lmbda, is_high, post_processing, pre_processing,
         if pre_processing:
             finetune_encoder(net, data, lmbda, tune_iter)
         with torch.no_grad():
-            eval_bpp, v_mse, v_psnr = net(data, 'test')
+            eval_bpp, v_mse, v_psnr = net(data, 'test', noise_seed=None if noise_seed is None else noise_seed + cnt)
         torch.cuda.synchronize()
         end_time = time.time()
         sum_time += end_time - begin_time
@@ -238,6 +238,9 @@ def main(argv=None):
     parser.add_argument("--arch", default="net_ga", choices=["net_ga", "net_unet_ha_hs"])
     parser.add_argument("--precision", default="fp32", choices=["fp32", "fp16"])
     parser.add_argument("--all-images", action="store_true", dest="all_images")
+    parser.add_argument("--noise_seed", type=int, default=None,
+                        help="price y + U(-1/2,1/2) as the reference's eval does (its nets are never put in "
+                             "eval mode); seeded, image k uses seed + k.  Default: dequantize semantics")
     parser.add_argument("--synthetic-kodak", action="store_true", dest="synthetic_kodak",
                         help="BASELINE config 4: R-D sweep over 24 synthetic Kodak-shaped images")
     parser.add_argument("--lambdas", default=",".join(str(v) for v in RD_LAMBDAS),
@@ -257,7 +260,8 @@ def main(argv=None):
         return
     print(args.weight_path)
     val(args.data_path, args.weight_path, args.lmbda, args.high, args.post_processing, args.pre_processing,
-        args.tune_iter, arch=args.arch, precision=args.precision, all_images=args.all_images)
+        args.tune_iter, arch=args.arch, precision=args.precision, all_images=args.all_images,
+        noise_seed=args.noise_seed)
 
 
 if __name__ == "__main__":

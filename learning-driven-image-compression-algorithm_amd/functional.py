@@ -432,6 +432,26 @@ def gauss_rate(y: Act, mu: Act, scale: Act, partials: torch.Tensor, part_off: in
     return n
 
 
+def rate_noise_parts(npix: int, c: int) -> int:
+    return int(_lib().lic_rate_train_parts(npix, c))
+
+
+def rate_noise(y: Act, mu: Act, scale: Act, seed: int, partials: torch.Tensor, part_off: int,
+               scale_bound: float = 0.11, likelihood_bound: float = 1e-9) -> int:
+    """compressai GaussianConditional.forward in its default (training) mode, as the reference's
+    eval runs it (the net is never put in eval(), net_ga.py:1049, eval_net.py:90-96): the
+    likelihood of y + U(-1/2, 1/2), with the counter-based noise of lic_rate_train_fwd
+    (seed, logical element index of the view).  Writes sum ln L partials at partials[part_off:]
+    and returns their count; y_hat / symbols are not touched (gauss_rate writes them)."""
+    n = rate_noise_parts(y.npix, y.c)
+    if part_off + n > partials.numel():
+        raise ValueError("rate_noise: partials buffer too small")
+    check(_lib().lic_rate_train_fwd(dtype_id(y.dtype), y.ptr, y.ld, mu.ptr, mu.ld, scale.ptr, scale.ld, y.npix, y.c,
+                                    int(seed) & 0xFFFFFFFFFFFFFFFF, scale_bound, likelihood_bound, None, 0,
+                                    _dp(partials) + part_off * 8, stream_handle()))
+    return n
+
+
 def bpp_finalize(partials: torch.Tensor, nparts: int, num_pixels: float, out: torch.Tensor,
                  sum_out: Optional[torch.Tensor] = None):
     check(_lib().lic_bpp_finalize(_dp(partials), nparts, float(num_pixels), _dp(out),

@@ -523,7 +523,7 @@ class Net(nn.Module):
         return LR, MU, SC, SYM, partials, nper
 
     def _slice_loop(self, z3: Optional[Act], MS: Act, SS: Act, LR: Act, MU: Act, SC: Act, SYM: torch.Tensor,
-                    LIK: Optional[torch.Tensor], partials: torch.Tensor, nper: int, decode=None):
+                    LIK: Optional[torch.Tensor], partials: torch.Tensor, nper: int, decode=None, noise=None):
         """net_ga.py:1028-1062.  Encoder / forward: y_i is quantised against mu_i and priced
         (lic_gauss_rate_fwd).  Decoder (``decode(i, mu, scale, yq_out, sym_out)``): the
         slice's symbols come from the bitstream instead of z3."""
@@ -554,6 +554,10 @@ class Net(nn.Module):
                               likelihood=Act(LIK, sw * i, sw) if LIK is not None else None,
                               scale_bound=self.gaussian_conditional._scale_bound,
                               likelihood_bound=self.gaussian_conditional._likelihood_bound)
+                if noise is not None:     # seeded-noise evaluation: the rate prices y + U(-1/2, 1/2)
+                    seed, nparts, nz = noise
+                    Fn.rate_noise(z3.ch(sw * i, sw * (i + 1)), mu, sc, seed * ns + i, nz, i * nparts,
+                                  self.gaussian_conditional._scale_bound, self.gaussian_conditional._likelihood_bound)
             else:
                 decode(i, mu, sc, yq, Act(SYM, sw * i, sw))
             lr = self.lrp_transforms[i]
@@ -669,7 +673,7 @@ class Net(nn.Module):
         return {"x_hat": x_rec, "symbols": SYM}
 
     def _forward_body(self, x_in: torch.Tensor, x_rec: torch.Tensor, partials: torch.Tensor, nper: int,
-                      sq_parts: torch.Tensor, ppi: int, return_intermediates: bool):
+                      sq_parts: torch.Tensor, ppi: int, return_intermediates: bool, noise=None):
         """encode -> quantize -> decode of a batch on the current stream (+ side streams);
         writes x_rec, the rate partials and the per-image squared-error partials."""
         B, _, H, W = x_in.shape
@@ -691,7 +695,7 @@ class Net(nn.Module):
         z, z_hat = self._hyper(z3, MS.ch(0, 192), SS.ch(0, 192))
         LR, MU, SC, SYM, _, _ = self._slice_buffers(B, hh, ww, dt, dev, with_partials=False)
         LIK = torch.empty((B, hh, ww, 192), dtype=torch.float32, device=dev) if return_intermediates else None
-        self._slice_loop(z3, MS, SS, LR, MU, SC, SYM, LIK, partials, nper)
+        self._slice_loop(z3, MS, SS, LR, MU, SC, SYM, LIK, partials, nper, noise=noise)
         y_hat = MS.ch(192, 384)
         x_tilde = self.s_model.run(y_hat)                          # net_ga.py:1078
         main.wait_stream(side)                                     # syntax head joined
@@ -726,10 +730,15 @@ class Net(nn.Module):
 
     # ---- forward
     def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False,
-                seed: Optional[int] = None):
-        """mode='test': (bpp, v_mse, v_psnr) (eval semantics, no autograd).  mode='train':
-        (bpp, mse) differentiable through liblic (lic_amd/train_net.py); ``seed`` picks the
-        GaussianConditional noise stream (default: a per-module counter)."""
+                seed: Optional[int] = None, noise_seed: Optional[int] = None):
+        """mode='test': (bpp, v_mse, v_psnr) (no autograd).  The rate uses eval ('dequantize')
+        semantics unless ``noise_seed`` is given: then it prices y + U(-1/2, 1/2) from that seed,
+        as the reference's eval does (its nets stay in training mode, net_ga.py:1049,
+        eval_net.py:90-96 -- torch's RNG there, a counter-based stream here, so the seeded
+        value is reproducible; symbols / y_hat / x_rec do not depend on it).
+        mode='train': (bpp, mse) differentiable through liblic (lic_amd/train_net.py); ``seed``
+        picks the GaussianConditional noise stream (default: a per-module counter); the same
+        seed gives the same noise as ``noise_seed`` in 'test'."""
         if not inputs.is_cuda:
             raise RuntimeError("lic_amd Net runs on the GPU only (HIP path); move inputs to cuda")
         if mode == 'train':
@@ -741,9 +750,9 @@ class Net(nn.Module):
         if mode != 'test':
             raise ValueError(f"mode must be 'train' or 'test', got {mode!r}")
         with torch.no_grad():
-            return self._forward_test(inputs, return_intermediates)
+            return self._forward_test(inputs, return_intermediates, noise_seed)
 
-    def _forward_test(self, inputs: torch.Tensor, return_intermediates: bool):
+    def _forward_test(self, inputs: torch.Tensor, return_intermediates: bool, noise_seed: Optional[int] = None):
         b, h, w, c = self.train_size
         x_in = inputs.contiguous().float()
         B, _, H, W = x_in.shape
@@ -756,10 +765,17 @@ class Net(nn.Module):
         ppi = max(1, min(64, -(-(H * W) // 4096)))
         sq_parts = torch.empty((B * ppi,), dtype=torch.float64, device=dev)
         x_rec = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
-        self._forward_body(x_in, x_rec, partials, nper, sq_parts, ppi, return_intermediates)
+        noise = None
+        if noise_seed is not None:
+            nz_per = Fn.rate_noise_parts(B * hh * ww, 192 // self.num_slices)
+            noise = (int(noise_seed), nz_per, torch.empty((self.num_slices * nz_per,), dtype=torch.float64, device=dev))
+        self._forward_body(x_in, x_rec, partials, nper, sq_parts, ppi, return_intermediates, noise)
         num_pixels = B * h * w
         bpp = torch.empty((1,), dtype=torch.float32, device=dev)
-        Fn.bpp_finalize(partials, self.num_slices * nper, num_pixels, bpp)  # :1134
+        if noise is None:
+            Fn.bpp_finalize(partials, self.num_slices * nper, num_pixels, bpp)  # :1134
+        else:
+            Fn.bpp_finalize(noise[2], self.num_slices * noise[1], num_pixels, bpp)
         v_mse = torch.empty((B,), dtype=torch.float32, device=dev)
         v_psnr = torch.empty((1,), dtype=torch.float32, device=dev)
         Fn.psnr_finalize(sq_parts, B, ppi, 3.0 * H * W, v_mse, v_psnr)

@@ -630,8 +630,27 @@ def han_head(x: Tensor, P: Params, pfx: str = "HAN", is_high: bool = False) -> T
 
 
 # --------------------------------------------------------------------------- full forward
-def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Params, num_slices: int = 4):
-    """Channel-conditional slice loop, net_ga.py:1021-1067 (eval / dequantize semantics)."""
+def counter_noise(seed: int, shape_nhwc) -> Tensor:
+    """U(-1/2, 1/2) of the seeded-noise rate (liblic's counter hash of (seed, NHWC element
+    index), train.hip noise_u): restated in numpy.  The reference draws the same
+    distribution from torch's RNG (compressai GaussianConditional 'noise' quantize), so the
+    stream itself is the build's own choice -- parity of this mode is pinned on it."""
+    n = int(np.prod(shape_nhwc))
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint64)
+        z = np.array([seed], dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + i
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    u = (z >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0) - np.float32(0.5)
+    return torch.from_numpy(u).view(*shape_nhwc)
+
+
+def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Params, num_slices: int = 4,
+               noise_seed=None):
+    """Channel-conditional slice loop, net_ga.py:1021-1067 (eval / dequantize semantics, or with
+    noise_seed the training-mode GaussianConditional the reference's eval actually runs:
+    likelihood of y + U(-1/2, 1/2))."""
     y_shape = z3.shape[2:]
     y_slices = z3.chunk(num_slices, 1)
     y_hat_slices: List[Tensor] = []
@@ -648,7 +667,11 @@ def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Param
         sc = _conv(gelu(_conv(gelu(_conv(ss, P, f"cc_scale_transforms.{i}.0", 1, 1)), P,
                                    f"cc_scale_transforms.{i}.2", 1, 1)), P, f"cc_scale_transforms.{i}.4", 1, 1)
         sc = sc[:, :, :y_shape[0], :y_shape[1]]
-        y_q = quantize_dequantize(y_slice, mu)
+        if noise_seed is None:
+            y_q = quantize_dequantize(y_slice, mu)
+        else:
+            B_, C_, H_, W_ = y_slice.shape
+            y_q = y_slice + counter_noise(noise_seed * num_slices + i, (B_, H_, W_, C_)).permute(0, 3, 1, 2)
         lik.append(gaussian_likelihood(y_q, sc, mu))
         syms.append(symbols(y_slice, mu))
         y_hat_slice = ste_round(y_slice - mu) + mu
@@ -666,7 +689,7 @@ def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Param
 
 @torch.no_grad()
 def net_forward(x: Tensor, P: Params, arch: str = "net_ga", train_hw=None, M: int = 16,
-                post_processing: bool = False, is_high: bool = False) -> Dict[str, Tensor]:
+                post_processing: bool = False, is_high: bool = False, noise_seed=None) -> Dict[str, Tensor]:
     """Net.forward(inputs, 'test') for arch in {'net_ga', 'net_unet_ha_hs'}:
     net_ga.py:981-1144 / net_unet_ha_hs.py:868-1032, eval (dequantize) semantics,
     visualisation / PNG side effects omitted.  Returns a dict of intermediates."""
@@ -689,7 +712,7 @@ def net_forward(x: Tensor, P: Params, arch: str = "net_ga", train_hw=None, M: in
         raise ValueError(arch)
     syn = syntax_model(z3[:, :M], P)
     syn_r = torch.round(syn)
-    y_hat, lik, syms, mus, scs = slice_loop(z3, latent_means, latent_scales, P)
+    y_hat, lik, syms, mus, scs = slice_loop(z3, latent_means, latent_scales, P, noise_seed=noise_seed)
     x_tilde = synthesis_transform(y_hat, P)
     cw = conv_generator(syn_r, P, "conv_weights_gen", M)
     x_bf = torch.tanh(batch_conv(cw, x_tilde))

@@ -118,3 +118,31 @@ def test_rd_sweep_runs_two_lambdas():
     assert ips > 0
     print(f"\n[rd sweep] {ips:.1f} images/s; " + "; ".join(f"{s['lambda']}: {s['bpp']:.4f} bpp {s['psnr']:.3f} dB"
                                                         for s in summ))
+
+
+@pytest.mark.parametrize("arch", ["net_ga", "net_unet_ha_hs"])
+def test_seeded_noise_eval_mode(arch):
+    """The reference's eval bpp is stochastic (its nets stay in training mode, so
+    GaussianConditional prices y + U(-1/2, 1/2): net_ga.py:1049, eval_net.py:90-96).
+    Net.forward(x, 'test', noise_seed=s) reproduces that mode with a seeded stream: bpp vs the
+    oracle with the same stream (1e-5), symbols / PSNR unchanged, another seed another bpp,
+    and the same seed in mode 'train' prices the same noisy values."""
+    net = _make(arch, "fp32")
+    P = {k: v.detach().float().cpu() for k, v in net.state_dict().items()}
+    net = net.to(DEV)
+    x = _input(1, 256, seed=31)
+    bpp0, _, psnr0 = net(x.to(DEV), "test")
+    bpp1, _, psnr1 = net(x.to(DEV), "test", return_intermediates=True, noise_seed=7)
+    sym1 = net.last["symbols"].cpu()
+    bpp2, _, _ = net(x.to(DEV), "test", noise_seed=8)
+    ref = R.net_forward(x, P, arch=arch, noise_seed=7)
+    print(f"\n[{arch} noise eval] bpp dequantize {bpp0.item():.6f} seed7 {bpp1.item():.6f} (ref {ref['bpp'].item():.6f}) "
+          f"seed8 {bpp2.item():.6f}")
+    assert abs(bpp1.item() - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item()))
+    assert check_symbols(sym1, ref) == 0
+    assert psnr1.item() == psnr0.item()
+    assert bpp1.item() != bpp0.item() and bpp2.item() != bpp1.item()
+    if arch == "net_ga":
+        with torch.no_grad():
+            bpp_t, _ = net(x.to(DEV), "train", seed=7)
+        assert abs(bpp_t.item() - bpp1.item()) <= 1e-4 * abs(bpp1.item())

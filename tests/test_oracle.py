@@ -181,3 +181,11 @@ def test_parity_check_symbols_accepts_only_near_ties():
     sym[0, 1, 12, 12] += 1                                   # no tie, no earlier flip nearby
     with _pt.raises(AssertionError):
         check_symbols(sym, ref, max_rate=1e-2)
+
+
+def test_counter_noise_is_uniform_and_seeded():
+    u = R.counter_noise(3, (2, 8, 8, 48))
+    assert u.shape == (2, 8, 8, 48) and u.min() >= -0.5 and u.max() < 0.5
+    assert abs(u.mean().item()) < 0.02 and abs(u.var().item() - 1 / 12) < 0.01
+    assert torch.equal(u, R.counter_noise(3, (2, 8, 8, 48)))
+    assert not torch.equal(u, R.counter_noise(4, (2, 8, 8, 48)))
