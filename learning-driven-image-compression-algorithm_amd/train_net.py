@@ -242,6 +242,66 @@ def generator(m, s):
     return linear(t[4], h)
 
 
+# --------------------------------------------------------------------------- net_unet_ha_hs hyper nets
+def _c(x):
+    return x.contiguous()
+
+
+def residual_block3_5(m, x):
+    """ResidualBlock3_5 (Block_unet.py:295-332): lrelu(conv3x3) lrelu(conv5x5) lrelu(conv3x3) + x."""
+    t = conv(m.conv1, x, ACT_LRELU)
+    t = conv(m.conv2, t, ACT_LRELU)
+    idn = conv(m.skip, x) if m.skip is not None else x
+    return AG.add(conv(m.conv3, t, ACT_LRELU), idn)
+
+
+def residual_block5x5(m, x):
+    """ResidualBlock5x5 (Block_unet.py:335-364): lrelu(conv5x5(x)) + x."""
+    idn = conv(m.skip, x) if m.skip is not None else x
+    return AG.add(conv(m.conv2, x, ACT_LRELU), idn)
+
+
+def residual_block3x3(m, x):
+    """ResidualBlock3x3 (Block_unet.py:367-398): lrelu(conv3x3) lrelu(conv3x3) + x."""
+    t = conv(m.conv1, x, ACT_LRELU)
+    idn = conv(m.skip, x) if m.skip is not None else x
+    return AG.add(conv(m.conv3, t, ACT_LRELU), idn)
+
+
+def conv_t1(m, x, act: int = ACT_NONE):
+    """nn.ConvTranspose2d without the ZeroPad2d pre-pad (Block_unet.py up1..up4)."""
+    return AG.conv_transpose2d(x, m.weight, m.bias, m.stride[0], m.padding[0], m.output_padding[0], (0, 0), act)
+
+
+def unet_ha_new(m, x):
+    """Unet_ha_new.forward (Block_unet.py:815-838) -> (z, middle_x, down_x1, x)."""
+    C = x.shape[-1]
+    h = C // 2
+    cat1 = torch.cat([residual_block3_5(m.conv1, _c(x[..., h:])), wba(m.SpatialTransformer1, _c(x[..., :h]))], -1)
+    d = AG.add(conv(m.down0, cat1), x)
+    down_x1 = conv(m.down1, d, ACT_GELU)
+    cat2 = torch.cat([residual_block5x5(m.conv2, _c(down_x1[..., :128])),
+                      wba(m.SpatialTransformer2, _c(down_x1[..., 128:]))], -1)
+    d2 = conv(m.down2, AG.add(conv(m.down3, cat2), down_x1), ACT_GELU)
+    mm = residual_bottleneck(m.middle[0], d2)
+    mm = wba(m.middle[1], mm)
+    mm = residual_bottleneck(m.middle[2], mm)
+    return mm, mm, down_x1, x
+
+
+def unet_hs_new(m, middle_x, down_x1, inp):
+    """Unet_hs_new.forward (Block_unet.py:868-890); its first argument (z_hat) is never read."""
+    cat0 = torch.cat([residual_block3x3(m.conv3, _c(middle_x[..., 256:])),
+                      wba(m.SpatialTransformer3, _c(middle_x[..., :256]))], -1)
+    u = AG.add(conv(m.up0, cat0), middle_x)
+    u1 = conv_t1(m.up3, torch.cat([conv_t1(m.up1, u, ACT_GELU), down_x1], -1), ACT_GELU)
+    cat2 = torch.cat([residual_block3x3(m.conv4, _c(u1[..., :128])), wba(m.SpatialTransformer2, _c(u1[..., 128:]))],
+                     -1)
+    u2 = AG.add(conv(m.up5, cat2), u1)
+    u2 = conv_t1(m.up2, u2, ACT_GELU)
+    return conv_t1(m.up4, torch.cat([u2, inp], -1))
+
+
 # --------------------------------------------------------------------------- Net
 def _cc(seq, x):
     """cc_mean / cc_scale / lrp transforms: conv3x3 GELU conv3x3 GELU conv3x3."""
@@ -249,9 +309,10 @@ def _cc(seq, x):
 
 
 def net_forward_train(net, inputs: torch.Tensor, seed: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """net_ga.Net.forward(inputs, 'train') -> (bpp, mse), differentiable through liblic."""
-    if net.arch != "net_ga":
-        raise NotImplementedError(f"train mode is implemented for net_ga (this is {net.arch})")
+    """net_ga.Net.forward(inputs, 'train') -> (bpp, mse), differentiable through liblic
+    (net_unet_ha_hs.Net: the U-Net hyper nets of net_unet_ha_hs.py:880-895)."""
+    if net.arch not in ("net_ga", "net_unet_ha_hs"):
+        raise NotImplementedError(f"train mode is not implemented for {net.arch}")
     if net.post_processing:
         raise NotImplementedError("train mode with post_processing (HAN) is not implemented")
     if not inputs.is_cuda:
@@ -264,10 +325,17 @@ def net_forward_train(net, inputs: torch.Tensor, seed: int) -> Tuple[torch.Tenso
     dev, dt = x_in.device, net.dtype
     x = AG.to_nhwc(x_in, dt)
     z3 = analysis(net.a_model, x)                                     # :988
-    z = seq_gelu(net.h_a, z3)                                         # :993
-    z_hat = AG.ste_quantize(z, net._medians(dev))                     # :996-1003
-    latent_scales = seq_gelu(net.h_scale_s, z_hat)                    # :1006
-    latent_means = seq_gelu(net.h_mean_s, z_hat)                      # :1007
+    if net.arch == "net_ga":
+        z = seq_gelu(net.h_a, z3)                                     # :993
+        z_hat = AG.ste_quantize(z, net._medians(dev))                 # :996-1003
+        latent_scales = seq_gelu(net.h_scale_s, z_hat)                # :1006
+        latent_means = seq_gelu(net.h_mean_s, z_hat)                  # :1007
+    else:
+        # net_unet_ha_hs.py:880-895: h_s reads encoder-side features, not z_hat, and the two
+        # identical h_s calls give latent_scales == latent_means (one call, its gradient sums
+        # both uses exactly as the reference's two calls do)
+        z, middle_x, down_x1, inp = unet_ha_new(net.h_a, z3)
+        latent_scales = latent_means = unet_hs_new(net.h_s, middle_x, down_x1, inp)
     syn = syntax(net.syntax_model, z3[..., :net.M].contiguous())      # :1013-1016
     cw = generator(net.conv_weights_gen, syn)                         # :1083
     sw = 192 // net.num_slices

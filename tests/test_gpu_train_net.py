@@ -93,16 +93,22 @@ def _rate_ref(y, mu, sc, seed, num_pixels):
     return bpp, yq.permute(0, 3, 1, 2)
 
 
-def _net_train_ref(x, P, seed, M=16, ns=4):
-    """net_ga.py:981-1115 in mode 'train' on the oracle, with the kernels' noise stream."""
+def _net_train_ref(x, P, seed, M=16, ns=4, arch="net_ga"):
+    """net_ga.py:981-1115 (net_unet_ha_hs.py:868-1003) in mode 'train' on the oracle, with the
+    kernels' noise stream."""
     B, _, H, W = x.shape
     num_pixels = B * H * W
     z3 = R.analysis_transform(x, P)
-    z = R.h_a_ga(z3, P)
-    med = P["entropy_bottleneck.quantiles"][:, :, 1:2].detach()
-    z_hat = R.ste_round(z - med) + med
-    latent_scales = R.h_s_ga(z_hat, P, "h_scale_s")
-    latent_means = R.h_s_ga(z_hat, P, "h_mean_s")
+    if arch == "net_ga":
+        z = R.h_a_ga(z3, P)
+        med = P["entropy_bottleneck.quantiles"][:, :, 1:2].detach()
+        z_hat = R.ste_round(z - med) + med
+        latent_scales = R.h_s_ga(z_hat, P, "h_scale_s")
+        latent_means = R.h_s_ga(z_hat, P, "h_mean_s")
+    else:
+        z, middle_x, down_x1, inp = R.unet_ha_new(z3, P)
+        latent_scales = R.unet_hs_new(middle_x, down_x1, inp, P)     # two calls, as the reference
+        latent_means = R.unet_hs_new(middle_x, down_x1, inp, P)
     syn = R.syntax_model(z3[:, :M], P)
     syn_r = syn + (torch.round(syn) - syn).detach()                     # bypass_round
     cc = lambda t, pfx: R._conv(R.gelu(R._conv(R.gelu(R._conv(t, P, pfx + ".0", 1, 1)), P, pfx + ".2", 1, 1)), P,
@@ -123,23 +129,27 @@ def _net_train_ref(x, P, seed, M=16, ns=4):
     return bpp, ((xt - x) ** 2).mean()
 
 
-def test_net_ga_train_step_fp32():
+@pytest.mark.parametrize("arch", ["net_ga", "net_unet_ha_hs"])
+def test_net_train_step_fp32(arch):
     """Net.forward(x, 'train') -> (bpp, mse), loss = lambda*255^2*mse + bpp (train_net_unet.py:180),
-    backward: loss terms and every parameter gradient vs the oracle's autograd."""
-    from lic_amd.model import net_ga
+    backward: loss terms and every parameter gradient vs the oracle's autograd (net_ga, and
+    net_unet_ha_hs with its U-Net hyper nets, Block_unet.py:774-890)."""
+    from lic_amd.model import net_ga, net_unet_ha_hs
     torch.manual_seed(0)
-    net = net_ga.synthetic_syntax_bias_(net_ga.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False, precision="fp32"))
+    mod = net_ga if arch == "net_ga" else net_unet_ha_hs
+    net = net_ga.synthetic_syntax_bias_(mod.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False, precision="fp32"))
     _lift_gammas(net)
     P = _params(net, "")
     x = torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(8)) * 2 - 1
     lmbda = 0.0025
-    bpp_r, mse_r = _net_train_ref(x, P, seed=5)
+    bpp_r, mse_r = _net_train_ref(x, P, seed=5, arch=arch)
     (lmbda * 255 ** 2 * mse_r + bpp_r).backward()
     net = net.to(DEV)
     bpp, mse = net(x.to(DEV), "train", seed=5)
     (lmbda * 255 ** 2 * mse + bpp).backward()
     torch.cuda.synchronize()
-    print(f"\n[train fp32] bpp {bpp.item():.6f} (ref {bpp_r.item():.6f}) mse {mse.item():.6e} (ref {mse_r.item():.6e})")
+    print(f"\n[{arch} train fp32] bpp {bpp.item():.6f} (ref {bpp_r.item():.6f}) mse {mse.item():.6e} "
+          f"(ref {mse_r.item():.6e})")
     assert abs(bpp.item() - bpp_r.item()) <= 1e-4 * abs(bpp_r.item())
     assert abs(mse.item() - mse_r.item()) <= 1e-4 * abs(mse_r.item())
     pairs = []
@@ -152,6 +162,9 @@ def test_net_ga_train_step_fp32():
     # the decoder is trained too (its gradient is zero when the rounded syntax is 0)
     assert sum(1 for n, _, _ in pairs if n.startswith("s_model.")) > 20
     assert sum(1 for n, _, _ in pairs if n.startswith("conv_weights_gen.")) >= 6
+    if arch == "net_unet_ha_hs":
+        assert sum(1 for n, _, _ in pairs if n.startswith("h_a.")) > 20
+        assert sum(1 for n, _, _ in pairs if n.startswith("h_s.")) > 20
     assert _grads_close(pairs) > 300
 
 
@@ -171,3 +184,57 @@ def test_eval_net_pre_processing_finetune():
     assert math.isfinite(bpp.item()) and math.isfinite(v_psnr.item())
     moved = {n for n, p in net.named_parameters() if not torch.equal(p.detach(), before[n])}
     assert moved and all(n.startswith("a_model.") for n in moved), sorted(moved)[:5]
+
+
+def test_pre_processing_finetune_trajectory():
+    """eval_net --pre_processing (eval_net.py:160-179): three online encoder
+    finetune steps (Adam(a_model, 1e-5), loss = lambda*mse + bpp in train mode) on the liblic
+    training path against the same three steps on the oracle's autograd with the same noise
+    streams (seeds 0, 1, 2 = the module's train-call counter).  Bar: the parameter updates of
+    every a_model tensor agree (Adam's normalised steps: median |d_gpu - d_ref| <= 1e-3 of the
+    3*lr step bound, 99th percentile <= 5e-2 -- an element whose gradient is ~0 may take the
+    other sign), only a_model moves, and a fresh train-mode loss after the finetune agrees
+    within 1e-4."""
+    import eval_net
+    from lic_amd.model import net_ga
+    torch.manual_seed(0)
+    net = net_ga.synthetic_syntax_bias_(net_ga.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False, precision="fp32"))
+    _lift_gammas(net)
+    P = {k: v.detach().clone().float() for k, v in net.state_dict().items()}
+    enc = [k for k, _ in net.named_parameters() if k.startswith("a_model.")]
+    for k in enc:
+        P[k].requires_grad_(True)
+    x = eval_net.synthetic_image(3, 256, 256).unsqueeze(0) * 2 - 1
+    lmbda, steps, lr = 0.0067, 3, 1e-5
+    opt = torch.optim.Adam([P[k] for k in enc], lr=lr)
+    sch = torch.optim.lr_scheduler.MultiStepLR(opt, [50], 0.5)
+    for s in range(steps):
+        bpp_r, mse_r = _net_train_ref(x, P, seed=s)
+        loss = (lmbda * mse_r + bpp_r).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        sch.step()
+    net = net.to(DEV)
+    before = {k: v.detach().clone() for k, v in net.named_parameters()}
+    eval_net.finetune_encoder(net, x.to(DEV), lmbda, steps)
+    torch.cuda.synchronize()
+    errs, moved = [], []
+    for k, p in net.named_parameters():
+        d_gpu = (p.detach() - before[k]).float().cpu()
+        if not k.startswith("a_model."):
+            assert torch.equal(p.detach(), before[k]), k
+            continue
+        d_ref = (P[k].detach() - before[k].float().cpu())
+        errs.append(((d_gpu - d_ref).abs() / (steps * lr)).flatten())
+        moved.append(bool(d_gpu.abs().max() > 0))
+    e = torch.cat(errs)
+    med, p99 = e.median().item(), e.quantile(0.99).item() if e.numel() < 2 ** 24 else e[::4].quantile(0.99).item()
+    print(f"\n[pre_processing x{steps}] {e.numel()} encoder weights: update error median {med:.2e}, p99 {p99:.2e} "
+          f"(units of {steps}*lr)")
+    assert all(moved) and med <= 1e-3 and p99 <= 5e-2
+    with torch.no_grad():
+        bpp_g, mse_g = net(x.to(DEV), "train", seed=99)
+        bpp_r, mse_r = _net_train_ref(x, {k: v.detach() for k, v in P.items()}, seed=99)
+    assert abs(bpp_g.item() - bpp_r.item()) <= 1e-4 * abs(bpp_r.item())
+    assert abs(mse_g.item() - mse_r.item()) <= 1e-4 * abs(mse_r.item())

@@ -7,8 +7,9 @@ What it does per step, as the reference (:167-200): ``bpp, mse = net(x, 'train')
 ``Adam(base_params)`` step; ``MultiStepLR([1500, 2500, 3500, 4000], 0.5)`` per epoch.
 
 Differences:
-  * the model is net_ga (eval_net.py's model): the reference script's ``model/Net_unet.py``
-    imports the missing ``model/Block.py`` and cannot be built;
+  * the model is ``--arch net_unet_ha_hs`` (default; SURVEY.md 2 row 17: the U-Net hyper-prior
+    net the script's name refers to) or net_ga (eval_net.py's model): the reference script's
+    ``model/Net_unet.py`` imports the missing ``model/Block.py`` and cannot be built;
   * one process per GPU (``torch.distributed.run``) with a bucketed gradient all-reduce
     overlapped with the backward (lic_amd.distributed.GradAllReduce, RCCL over xGMI)
     instead of single-process ``nn.DataParallel`` (:152);
@@ -69,6 +70,7 @@ def main():
     ap.add_argument("--batch_size", type=float, default=8, help="images per GPU")
     ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     ap.add_argument("--crop", type=int, default=256)
+    ap.add_argument("--arch", default="net_unet_ha_hs", choices=["net_unet_ha_hs", "net_ga"])
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--steps_per_epoch", type=int, default=20)
     ap.add_argument("--log_every", type=int, default=10)
@@ -79,15 +81,16 @@ def main():
     args = ap.parse_args()
 
     from lic_amd import distributed as D
-    from lic_amd.model import net_ga
+    from lic_amd.model import net_ga, net_unet_ha_hs
     rank, world, local = D.init("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B = int(args.batch_size)
 
     torch.manual_seed(0)
-    net = net_ga.Net((B, args.crop, args.crop, 3), (1, args.crop, args.crop, 3), args.high, args.post_processing,
-                     precision=args.precision)
+    mod = net_ga if args.arch == "net_ga" else net_unet_ha_hs
+    net = mod.Net((B, args.crop, args.crop, 3), (1, args.crop, args.crop, 3), args.high, args.post_processing,
+                  precision=args.precision)
     if args.weight_path:
         net.load_state_dict(torch.load(args.weight_path, map_location="cpu", weights_only=True), strict=True)
     net = net.to(dev)
@@ -128,13 +131,13 @@ def main():
         last = float(out[0])
         if rank == 0:
             print(json.dumps({
-                "metric": f"train images/sec ({args.crop}x{args.crop} crops, net_ga, batch {B}/GPU)",
+                "metric": f"train images/sec ({args.crop}x{args.crop} crops, {args.arch}, batch {B}/GPU)",
                 "value": round(world * B * args.steps / dt, 2), "unit": "images/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                 "dtype": "f16" if args.precision == "fp16" else "f32",
                 "data": "synthetic (seeded smooth images, random crops in HBM; no DIV2K)",
-                "config": {"workload": "net_ga Net.forward(x,'train') + backward + grad all-reduce + clip + Adam",
+                "config": {"workload": f"{args.arch} Net.forward(x,'train') + backward + grad all-reduce + clip + Adam",
                            "global_batch": world * B, "crop": args.crop, "lambda": args.lmbda,
                            "parallelism": f"data-parallel x{world} (bucketed RCCL all-reduce)"},
                 "loss_first_last": [round(first, 4), round(last, 4)]}), flush=True)
