@@ -33,7 +33,7 @@ extern "C" {
 
 typedef void* lic_stream_t; /* hipStream_t */
 
-enum lic_dtype { LIC_F32 = 0, LIC_F16 = 1 };
+enum lic_dtype { LIC_F32 = 0, LIC_F16 = 1, LIC_BF16 = 2 };
 enum lic_act { LIC_ACT_NONE = 0, LIC_ACT_RELU = 1, LIC_ACT_LRELU = 2, LIC_ACT_GELU = 3, LIC_ACT_ROUND = 4 };
 enum lic_prologue { LIC_PRO_NONE = 0, LIC_PRO_SQUARE = 1, LIC_PRO_ABS = 2 };
 enum lic_epilogue {

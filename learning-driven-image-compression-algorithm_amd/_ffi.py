@@ -13,7 +13,7 @@ import pathlib
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "liblic.so"
 
-LIC_F32, LIC_F16 = 0, 1
+LIC_F32, LIC_F16, LIC_BF16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_GELU, ACT_ROUND = 0, 1, 2, 3, 4
 PRO_NONE, PRO_SQUARE, PRO_ABS = 0, 1, 2
 EPI_PLAIN, EPI_GATE, EPI_HALF_TANH, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, EPI_RES_ACT = 0, 1, 2, 3, 4, 5, 6

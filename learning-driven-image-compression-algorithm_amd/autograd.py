@@ -13,7 +13,7 @@ the same through ``a_model``).  Every gradient here is a liblic launch:
   ``lic_act_bwd``, ``lic_gdn_bwd_elem`` + ``lic_gdn_bwd_finish``,
   ``lic_lower_bound_sq_bwd``.
 
-Tensors are NHWC ``[B, H, W, C]`` contiguous, fp32 (parity) or fp16; weights are the
+Tensors are NHWC ``[B, H, W, C]`` contiguous, fp32 (parity), fp16 or bf16; weights are the
 fp32 ``nn.Parameter``s in the reference's layouts (Conv2d ``[co, ci, kh, kw]``,
 ConvTranspose2d ``[ci, co, kh, kw]``, GDN ``beta [C]`` / ``gamma [C, C]``), and their
 gradients come back fp32 in those layouts.  There is no PyTorch compute fallback.

@@ -186,5 +186,6 @@ extern "C" int lic_win_attn_fwd(const lic_attn_args* a, lic_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == LIC_F32) return attn_dispatch<float>(*a, s);
   if (a->dtype == LIC_F16) return attn_dispatch<half_t>(*a, s);
+  if (a->dtype == LIC_BF16) return attn_dispatch<bf16_t>(*a, s);
   return fail("attn: bad dtype");
 }

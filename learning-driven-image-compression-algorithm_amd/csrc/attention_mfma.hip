@@ -60,7 +60,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
   const int qoff = hc * d, koff = a.c + hc * d, voff = 2 * a.c + hc * d;
   // fp16: K/Q fragments straight from the qkv map (lane (row, h) holds channels
   // 16s + 8h .. +7), issued before the V^T staging so all reads are in flight at once
-  half8 kf[2][2] = {}, qf[2][2] = {};
+  u32x4 kf[2][2] = {}, qf[2][2] = {};
   if constexpr (sizeof(T) == 2) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -69,8 +69,8 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2) {
         const T* tp = qkv + (int64_t)(t2 ? pix_lr1 : pix_lr0) * ldq;
-        kf[s][t2] = *(const half8*)(tp + koff + ch);
-        qf[s][t2] = *(const half8*)(tp + qoff + ch);
+        kf[s][t2] = *(const u32x4*)(tp + koff + ch);
+        qf[s][t2] = *(const u32x4*)(tp + qoff + ch);
       }
     }
   }
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
       for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
-          S[tj][ti] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[s][tj], qf[s][ti], S[tj][ti], 0, 0, 0);
+          S[tj][ti] = mfma_k16<T>(kf[s][tj], qf[s][ti], S[tj][ti]);
     }
   } else {
     for (int k = 0; k < d; k += 2) {
@@ -207,15 +207,16 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int j0 = 32 * tj + 16 * s2 + 4 * lh;
-        half8 va;
+        u32x4 va;
         *(uint2*)&va = *(const uint2*)(vrow + j0);
         *((uint2*)&va + 1) = *(const uint2*)(vrow + j0 + 8);
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti) {
-          half8 pb;
+          u32x4 pb;
+          T* pe = (T*)&pb;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) pb[e] = (half_t)S[tj][ti][8 * s2 + e];
-          O[ti] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pb, O[ti], 0, 0, 0);
+          for (int e = 0; e < 8; ++e) pe[e] = from_f<T>(S[tj][ti][8 * s2 + e]);
+          O[ti] = mfma_k16<T>(va, pb, O[ti]);
         }
       }
   } else {
@@ -244,9 +245,9 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
       if (c0 >= d) continue;
       if constexpr (sizeof(T) == 2) {
         uint2 pk;
-        half_t* e = (half_t*)&pk;
+        T* e = (T*)&pk;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) e[k] = (half_t)O[ti][4 * g + k];
+        for (int k = 0; k < 4; ++k) e[k] = from_f<T>(O[ti][4 * g + k]);
         *(uint2*)(op + c0) = pk;
       } else {
         *(float4*)(op + c0) = make_float4(O[ti][4 * g], O[ti][4 * g + 1], O[ti][4 * g + 2], O[ti][4 * g + 3]);
@@ -263,11 +264,14 @@ int win_attn_mfma_dispatch(const lic_attn_args& a, hipStream_t s, int& status) {
   // one L2; 64x64 WBA 97 -> 77 us).  Small maps keep 4 waves for more workgroups, fp32
   // for the LDS (its V^T image is twice the size)
   const int64_t windows = (int64_t)a.n * (a.h / 8) * (a.w / 8);
-  const int nw = (a.dtype == LIC_F16 && a.heads >= 8 && windows >= 1024) ? 8 : 4;
+  const int nw = (a.dtype != LIC_F32 && a.heads >= 8 && windows >= 1024) ? 8 : 4;
   const int64_t blocks = windows * ((a.heads + nw - 1) / nw);
   if (a.dtype == LIC_F16) {
     if (nw == 8) hipLaunchKernelGGL((win_attn_mfma_kernel<half_t, 8>), dim3((unsigned)blocks), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((win_attn_mfma_kernel<half_t, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  } else if (a.dtype == LIC_BF16) {
+    if (nw == 8) hipLaunchKernelGGL((win_attn_mfma_kernel<bf16_t, 8>), dim3((unsigned)blocks), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((win_attn_mfma_kernel<bf16_t, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL((win_attn_mfma_kernel<float, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   }

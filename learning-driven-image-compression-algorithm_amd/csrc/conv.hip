@@ -198,5 +198,6 @@ extern "C" int lic_conv2d_fwd(const lic_conv_args* a, lic_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == LIC_F32) return conv_dispatch<float>(*a, s);
   if (a->dtype == LIC_F16) return conv_dispatch<half_t>(*a, s);
+  if (a->dtype == LIC_BF16) return conv_dispatch<bf16_t>(*a, s);
   return fail("conv: bad dtype");
 }

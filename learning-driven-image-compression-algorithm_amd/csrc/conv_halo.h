@@ -231,8 +231,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(const lic_conv_
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (sizeof(T) == 2) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&fa[i], *(const half8*)&fb[j],
-                                                               acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma_k16<T>(fa[i], fb[j], acc[i][j]);
           } else {
             const float* af = (const float*)&fa[i];
             const float* bf = (const float*)&fb[j];

@@ -172,9 +172,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (sizeof(T) == 2) {
-            half8 av = *(half8*)&fa[i];
-            half8 bv = *(half8*)&fb[j];
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma_k16<T>(fa[i], fb[j], acc[i][j]);
           } else {
             const float* af = (const float*)&fa[i];
             const float* bf = (const float*)&fb[j];

@@ -142,6 +142,8 @@ extern "C" int lic_gauss_rate_fwd(const lic_rate_args* a, lic_stream_t stream) {
     hipLaunchKernelGGL(gauss_rate_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, *a);
   else if (a->dtype == LIC_F16)
     hipLaunchKernelGGL(gauss_rate_kernel<half_t>, dim3((unsigned)blocks), dim3(256), 0, s, *a);
+  else if (a->dtype == LIC_BF16)
+    hipLaunchKernelGGL(gauss_rate_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, s, *a);
   else
     return fail("rate: bad dtype");
   LIC_CHECK_LAUNCH();
@@ -161,6 +163,9 @@ extern "C" int lic_quantize_median(int32_t dtype, const void* z, int32_t npix, i
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(quantize_median_kernel<half_t>, dim3(blocks), dim3(256), 0, s, (const half_t*)z, npix, c, ldz,
                        medians, (half_t*)out, ldo);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(quantize_median_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)z, npix, c, ldz,
+                       medians, (bf16_t*)out, ldo);
   else
     return fail("quantize: bad dtype");
   LIC_CHECK_LAUNCH();
@@ -190,6 +195,9 @@ extern "C" int lic_syntax_recon_fwd(int32_t dtype, const void* xtil, int32_t n, 
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(syntax_recon_kernel<half_t>, grid, dim3(256), 0, s, (const half_t*)xtil, h, w, cin, ldx, ldw,
                        (const half_t*)wgen, x, x_rec, sqerr_partials, parts_per_img);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(syntax_recon_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)xtil, h, w, cin, ldx, ldw,
+                       (const bf16_t*)wgen, x, x_rec, sqerr_partials, parts_per_img);
   else
     return fail("recon: bad dtype");
   LIC_CHECK_LAUNCH();

@@ -403,6 +403,13 @@ extern "C" int lic_pool_partials(int32_t dtype, const void* x, int32_t ldx, int3
     else
       hipLaunchKernelGGL((pool_partials_kernel<half_t, false>), grid, dim3(256), 0, s, (const half_t*)x, ldx, hw, c,
                          nchunk, parts);
+  } else if (dtype == LIC_BF16) {
+    if (vec_ok<bf16_t>(x, ldx, c))
+      hipLaunchKernelGGL((pool_partials_kernel<bf16_t, true>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, hw, c,
+                         nchunk, parts);
+    else
+      hipLaunchKernelGGL((pool_partials_kernel<bf16_t, false>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, hw, c,
+                         nchunk, parts);
   } else {
     return fail("pool_partials: bad dtype");
   }
@@ -438,6 +445,9 @@ extern "C" int lic_ca_apply_fwd(int32_t dtype, const void* r, int32_t ldr, const
   } else if (dtype == LIC_F16) {
     const bool v = vec_ok<half_t>(r, ldr, c) && vec_ok<half_t>(x, ldx, c) && vec_ok<half_t>(out, ldo, c);
     ca_launch<half_t>(v, grid, s, r, ldr, x, ldx, hw, c, y, out, ldo);
+  } else if (dtype == LIC_BF16) {
+    const bool v = vec_ok<bf16_t>(r, ldr, c) && vec_ok<bf16_t>(x, ldx, c) && vec_ok<bf16_t>(out, ldo, c);
+    ca_launch<bf16_t>(v, grid, s, r, ldr, x, ldx, hw, c, y, out, ldo);
   } else {
     return fail("ca_apply: bad dtype");
   }
@@ -469,6 +479,11 @@ static int lam_launch(int32_t dtype, const void* x, int32_t ldx, int32_t n, int3
       lam_launch_t<half_t, N, true>(x, ldx, n, hw, C, parts, nblk, gamma, out, ldo, s);
     else
       lam_launch_t<half_t, N, false>(x, ldx, n, hw, C, parts, nblk, gamma, out, ldo, s);
+  } else if (dtype == LIC_BF16) {
+    if (vec_ok<bf16_t>(x, ldx, C) && vec_ok<bf16_t>(out, ldo, C))
+      lam_launch_t<bf16_t, N, true>(x, ldx, n, hw, C, parts, nblk, gamma, out, ldo, s);
+    else
+      lam_launch_t<bf16_t, N, false>(x, ldx, n, hw, C, parts, nblk, gamma, out, ldo, s);
   } else {
     return fail("lam: bad dtype");
   }
@@ -510,6 +525,9 @@ extern "C" int lic_csam_fwd(int32_t dtype, const void* x, int32_t ldx, int32_t n
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(csam_kernel<half_t>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, ldx, n, h, w, c, params,
                        (half_t*)out, ldo);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(csam_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)x, ldx, n, h, w, c, params,
+                       (bf16_t*)out, ldo);
   else
     return fail("csam: bad dtype");
   LIC_CHECK_LAUNCH();
@@ -533,6 +551,10 @@ extern "C" int lic_recon_fwd(int32_t dtype, const void* xtil, int32_t n, int32_t
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(recon_kernel<half_t>, grid, dim3(256), 0, s, (const half_t*)xtil, h, w, cin, ldx, ldw,
                        (const half_t*)wgen, mode, post, x, x_rec, sqerr_partials, parts_per_img, (half_t*)y, ldy,
+                       ycpad);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(recon_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)xtil, h, w, cin, ldx, ldw,
+                       (const bf16_t*)wgen, mode, post, x, x_rec, sqerr_partials, parts_per_img, (bf16_t*)y, ldy,
                        ycpad);
   else
     return fail("recon: bad dtype");

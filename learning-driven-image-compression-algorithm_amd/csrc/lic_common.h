@@ -9,6 +9,8 @@ namespace lic {
 
 typedef _Float16 half_t;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -31,12 +33,25 @@ hipError_t ensure_dyn_lds(const void* kern, int bytes);
 template <typename T> struct DT;
 template <> struct DT<float> { static constexpr int id = LIC_F32; };
 template <> struct DT<half_t> { static constexpr int id = LIC_F16; };
+template <> struct DT<bf16_t> { static constexpr int id = LIC_BF16; };
 
 __device__ __forceinline__ float to_f(float v) { return v; }
 __device__ __forceinline__ float to_f(half_t v) { return (float)v; }
+__device__ __forceinline__ float to_f(bf16_t v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ half_t from_f<half_t>(float v) { return (half_t)v; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return (bf16_t)v; }   // RNE
+
+// One 32x32x16 MFMA on 16-bit operands (8 per lane, as 16 raw bytes): fp16 or bf16 by T,
+// fp32 accumulation.  v_mfma_f32_32x32x16_{f16,bf16}.
+template <typename T>
+__device__ __forceinline__ floatx16 mfma_k16(const u32x4& a, const u32x4& b, const floatx16& c) {
+  if constexpr (DT<T>::id == LIC_BF16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(*(const bf16x8*)&a, *(const bf16x8*)&b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const half8*)&a, *(const half8*)&b, c, 0, 0, 0);
+}
 
 // exact (erf) GELU, nn.GELU() default
 __device__ __forceinline__ float gelu_f(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }

@@ -86,6 +86,9 @@ using namespace lic;
     } else if ((dtype) == LIC_F16) {                                   \
       typedef half_t T;                                                \
       __VA_ARGS__;                                                     \
+    } else if ((dtype) == LIC_BF16) {                                  \
+      typedef bf16_t T;                                                \
+      __VA_ARGS__;                                                     \
     } else                                                             \
       return fail(std::string(NAME) + ": bad dtype");                  \
   } while (0)
@@ -143,6 +146,15 @@ extern "C" int lic_copy(int32_t dtype_in, const void* x, int32_t ldx, int32_t np
   else if (dtype_in == LIC_F16 && dtype_out == LIC_F16)
     hipLaunchKernelGGL((copy_kernel<half_t, half_t>), dim3(nblk(total)), dim3(256), 0, s, (const half_t*)x, ldx, npix,
                        c, (half_t*)y, ldy);
+  else if (dtype_in == LIC_F32 && dtype_out == LIC_BF16)
+    hipLaunchKernelGGL((copy_kernel<float, bf16_t>), dim3(nblk(total)), dim3(256), 0, s, (const float*)x, ldx, npix, c,
+                       (bf16_t*)y, ldy);
+  else if (dtype_in == LIC_BF16 && dtype_out == LIC_F32)
+    hipLaunchKernelGGL((copy_kernel<bf16_t, float>), dim3(nblk(total)), dim3(256), 0, s, (const bf16_t*)x, ldx, npix,
+                       c, (float*)y, ldy);
+  else if (dtype_in == LIC_BF16 && dtype_out == LIC_BF16)
+    hipLaunchKernelGGL((copy_kernel<bf16_t, bf16_t>), dim3(nblk(total)), dim3(256), 0, s, (const bf16_t*)x, ldx, npix,
+                       c, (bf16_t*)y, ldy);
   else
     return fail("copy: bad dtype");
   LIC_CHECK_LAUNCH();

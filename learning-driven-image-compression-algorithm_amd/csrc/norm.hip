@@ -69,6 +69,9 @@ extern "C" int lic_gdn_prepare(int32_t dtype, const float* beta, const float* ga
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(gdn_prepare_kernel<half_t>, dim3(blocks), dim3(256), 0, s, beta, gamma, c, beta_bound,
                        gamma_bound, pedestal, (half_t*)wgt_out, cpad, copad, beta_out);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(gdn_prepare_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, beta, gamma, c, beta_bound,
+                       gamma_bound, pedestal, (bf16_t*)wgt_out, cpad, copad, beta_out);
   else
     return fail("gdn_prepare: bad dtype");
   LIC_CHECK_LAUNCH();
@@ -88,6 +91,9 @@ extern "C" int lic_layernorm_fwd(int32_t dtype, const void* x, int32_t npix, int
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(layernorm_kernel<half_t>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, npix, c, ldx,
                        weight, bias, eps, (half_t*)y, ldy);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(layernorm_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)x, npix, c, ldx,
+                       weight, bias, eps, (bf16_t*)y, ldy);
   else
     return fail("layernorm: bad dtype");
   LIC_CHECK_LAUNCH();

@@ -503,6 +503,9 @@ extern "C" int lic_gauss_indexes(int32_t dtype, const void* scales, int32_t npix
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(gauss_indexes_kernel<half_t>, dim3(blocks), dim3(256), 0, s, (const half_t*)scales, npix, c,
                        ldsc, scale_table, ntab, bound, idx, ldidx);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(gauss_indexes_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)scales, npix, c,
+                       ldsc, scale_table, ntab, bound, idx, ldidx);
   else
     return fail("gauss_indexes: bad dtype");
   LIC_CHECK_LAUNCH();
@@ -520,6 +523,9 @@ extern "C" int lic_quantize_symbols(int32_t dtype, const void* z, int32_t npix, 
                        medians, sym, ldsym);
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(quantize_symbols_kernel<half_t>, dim3(blocks), dim3(256), 0, s, (const half_t*)z, npix, c, ldz,
+                       medians, sym, ldsym);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(quantize_symbols_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)z, npix, c, ldz,
                        medians, sym, ldsym);
   else
     return fail("quantize_symbols: bad dtype");
@@ -569,7 +575,9 @@ extern "C" int lic_rans_decode(const lic_rans_args* a, lic_stream_t stream) {
   const int64_t worst = (int64_t)a->ncdf * a->cdf_stride;
   const int lds_words = a->ncdf <= kDecMaxStagedTables ? (int)(worst < kDecLdsWords ? worst : kDecLdsWords) : 0;
   const size_t lds = (size_t)lds_words * sizeof(int32_t);
-  const void* kern = a->dtype == LIC_F32 ? (const void*)rans_decode_kernel<float> : (const void*)rans_decode_kernel<half_t>;
+  const void* kern = a->dtype == LIC_F32   ? (const void*)rans_decode_kernel<float>
+                     : a->dtype == LIC_BF16 ? (const void*)rans_decode_kernel<bf16_t>
+                                            : (const void*)rans_decode_kernel<half_t>;
   const hipError_t ea = ensure_dyn_lds(kern, kDecLdsWords * 4);
   if (ea != hipSuccess) return fail(std::string("rans_decode: dynamic LDS attribute: ") + hipGetErrorString(ea));
   const dim3 grid((unsigned)((ns + 63) / 64));
@@ -577,6 +585,8 @@ extern "C" int lic_rans_decode(const lic_rans_args* a, lic_stream_t stream) {
     hipLaunchKernelGGL(rans_decode_kernel<float>, grid, dim3(64), lds, s, *a, lds_words);
   else if (a->dtype == LIC_F16)
     hipLaunchKernelGGL(rans_decode_kernel<half_t>, grid, dim3(64), lds, s, *a, lds_words);
+  else if (a->dtype == LIC_BF16)
+    hipLaunchKernelGGL(rans_decode_kernel<bf16_t>, grid, dim3(64), lds, s, *a, lds_words);
   else
     return fail("rans_decode: bad dtype");
   LIC_CHECK_LAUNCH();

@@ -63,6 +63,9 @@ extern "C" int lic_rb3_fwd(int32_t dtype, const void* x, int32_t n, int32_t h, i
   else if (dtype == LIC_F16)
     hipLaunchKernelGGL(rb3_kernel<half_t>, dim3(blocks), dim3(256), 0, s, (const half_t*)x, n, h, w, ldx, params,
                        (half_t*)y, ldy);
+  else if (dtype == LIC_BF16)
+    hipLaunchKernelGGL(rb3_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)x, n, h, w, ldx, params,
+                       (bf16_t*)y, ldy);
   else
     return fail("rb3: bad dtype");
   LIC_CHECK_LAUNCH();

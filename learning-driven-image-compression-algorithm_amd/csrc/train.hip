@@ -141,9 +141,7 @@ __global__ __launch_bounds__(WM * WN * 64) void wgrad_kernel(const lic_wgrad_arg
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (sizeof(T) == 2) {
-            half8 av = *(half8*)&fa[i];
-            half8 bv = *(half8*)&fb[j];
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma_k16<T>(fa[i], fb[j], acc[i][j]);
           } else {
             const float* af = (const float*)&fa[i];
             const float* bf = (const float*)&fb[j];
@@ -222,7 +220,7 @@ static WgPlan wgrad_plan(const lic_wgrad_args& a) {
   p.tiles_m = (a.co + p.bm - 1) / p.bm;
   p.tiles_n = (a.ci + p.bn - 1) / p.bn;
   p.K = a.n * a.mi * a.mj;
-  const int bk = a.dtype == LIC_F16 ? 32 : 16;
+  const int bk = a.dtype != LIC_F32 ? 32 : 16;
   const int per_split = p.tiles_m * p.tiles_n * a.ntaps;
   const int max_split = std::max(1, (p.K + 8 * bk - 1) / (8 * bk));  // >= 8 K steps per work-group
   int ns = std::max(1, (2048 + per_split - 1) / per_split);
@@ -235,8 +233,9 @@ static WgPlan wgrad_plan(const lic_wgrad_args& a) {
 }
 
 static int wgrad_check(const lic_wgrad_args& a) {
-  if (a.dtype != LIC_F32 && a.dtype != LIC_F16) return fail("wgrad: dtype must be LIC_F32 or LIC_F16");
-  const int epc = a.dtype == LIC_F16 ? 8 : 4;
+  if (a.dtype != LIC_F32 && a.dtype != LIC_F16 && a.dtype != LIC_BF16)
+    return fail("wgrad: dtype must be LIC_F32, LIC_F16 or LIC_BF16");
+  const int epc = a.dtype != LIC_F32 ? 8 : 4;
   if (!a.x || !a.dz || !a.dw) return fail("wgrad: null pointer");
   if (a.ci <= 0 || a.co <= 0 || a.n <= 0 || a.mi <= 0 || a.mj <= 0) return fail("wgrad: empty problem");
   if (a.ci % epc || a.co % epc || a.ldx % epc || a.ldz % epc)
@@ -907,8 +906,11 @@ using namespace lic;
     } else if ((dtype) == LIC_F16) {                                    \
       typedef half_t T;                                                 \
       __VA_ARGS__;                                                      \
+    } else if ((dtype) == LIC_BF16) {                                   \
+      typedef bf16_t T;                                                 \
+      __VA_ARGS__;                                                      \
     } else                                                              \
-      return fail(std::string(NAME) + ": dtype must be LIC_F32 or LIC_F16"); \
+      return fail(std::string(NAME) + ": dtype must be LIC_F32, LIC_F16 or LIC_BF16"); \
   } while (0)
 
 static inline unsigned tr_nblk(int64_t total) { return (unsigned)((total + 255) / 256); }
@@ -931,6 +933,9 @@ extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {
   if (a.dtype == LIC_F16) {
     if (p.bm == 128) wgrad_launch<half_t, 128, 128, 2, 2>(a, p, s);
     else wgrad_launch<half_t, 64, 64, 2, 2>(a, p, s);
+  } else if (a.dtype == LIC_BF16) {
+    if (p.bm == 128) wgrad_launch<bf16_t, 128, 128, 2, 2>(a, p, s);
+    else wgrad_launch<bf16_t, 64, 64, 2, 2>(a, p, s);
   } else {
     if (p.bm == 128) wgrad_launch<float, 128, 128, 2, 2>(a, p, s);
     else wgrad_launch<float, 64, 64, 2, 2>(a, p, s);

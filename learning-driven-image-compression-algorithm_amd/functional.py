@@ -17,14 +17,14 @@ import torch
 from . import _ffi
 from ._ffi import ConvArgs, AttnArgs, RateArgs, check
 
-_DT = {torch.float32: _ffi.LIC_F32, torch.float16: _ffi.LIC_F16}
+_DT = {torch.float32: _ffi.LIC_F32, torch.float16: _ffi.LIC_F16, torch.bfloat16: _ffi.LIC_BF16}
 
 
 def dtype_id(dt: torch.dtype) -> int:
     try:
         return _DT[dt]
     except KeyError:
-        raise _ffi.LicError(f"unsupported activation dtype {dt}; use float32 or float16")
+        raise _ffi.LicError(f"unsupported activation dtype {dt}; use float32, float16 or bfloat16")
 
 
 def stream_handle() -> int:
@@ -155,7 +155,7 @@ def _choose_copad(co: int) -> int:
 
 
 def _cpad_for(ci: int, dtype: torch.dtype) -> int:
-    bk = 32 if dtype == torch.float16 else 16
+    bk = 32 if dtype != torch.float32 else 16
     return -(-ci // bk) * bk
 
 
@@ -168,7 +168,7 @@ def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
     cin = cig if cin_to is None else cin_to
     # channel counts the MFMA kernel cannot take (not a multiple of one 16-byte chunk, or
     # grouped) go to the direct kernel, which wants the weights unpadded
-    epc = 8 if dtype == torch.float16 else 4
+    epc = 8 if dtype != torch.float32 else 4
     cpad = _cpad_for(cin, dtype) if (groups == 1 and cin % epc == 0) else cin
     copad = _choose_copad(co)
     # one permute+cast copy kernel (plus a fill when padded): the training path re-packs

@@ -358,7 +358,8 @@ _IGNORED_PREFIXES = ("y_sampler.", "h_sampler.", "test_y_sampler.", "test_h_samp
 
 class Net(nn.Module):
     """net_ga.Net (net_ga.py:735-1144).  ``precision`` selects the activation dtype of
-    the HIP path: 'fp32' (parity) or 'fp16' (fp32 accumulation)."""
+    the HIP path: 'fp32' (parity), 'fp16' or 'bf16' (fp32 accumulation; bf16 is the training
+    precision of BASELINE config 5)."""
 
     arch = "net_ga"
 
@@ -372,6 +373,8 @@ class Net(nn.Module):
         self.test_size = test_size
         self.post_processing = post_processing
         self.is_high = is_high
+        if precision not in ("fp32", "fp16", "bf16"):
+            raise ValueError(f"precision must be 'fp32', 'fp16' or 'bf16', got {precision!r}")
         self.precision = precision
         N, M = (384, 32) if is_high else (192, 16)
         self.M, self.N = M, N
@@ -509,7 +512,7 @@ class Net(nn.Module):
 
     @property
     def dtype(self):
-        return torch.float16 if self.precision == "fp16" else torch.float32
+        return {"fp16": torch.float16, "bf16": torch.bfloat16}.get(self.precision, torch.float32)
 
     def _slice_buffers(self, B, hh, ww, dt, dev, with_partials: bool = True):
         sw = 192 // self.num_slices

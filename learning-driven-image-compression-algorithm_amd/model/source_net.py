@@ -83,7 +83,7 @@ class Net(nn.Module):
         self.h_a = h_analysisTransformModel(N, [N, N, N], [1, 2, 2])
 
     def _dtype(self):
-        return torch.float16 if self.precision == "fp16" else torch.float32
+        return {"fp16": torch.float16, "bf16": torch.bfloat16}.get(self.precision, torch.float32)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         sd = {k: v for k, v in state_dict.items() if k.startswith(("a_model.", "h_a."))}

@@ -22,10 +22,11 @@ def _P(module, prefix=""):
 def _close(out, ref, dtype, rtol=1e-4, atol=1e-4):
     out = out.float().cpu()
     ref = ref.float().cpu()
-    if dtype == torch.float16:
+    if dtype != torch.float32:   # 16-bit activations: fp16 2e-2, bf16 4e-2 of the scale
         scale = ref.abs().max().item() + 1e-6
         err = (out - ref).abs().max().item()
-        assert err <= 2e-2 * scale, f"fp16 max err {err} vs scale {scale}"
+        tol = 2e-2 if dtype == torch.float16 else 4e-2
+        assert err <= tol * scale, f"{dtype} max err {err} vs scale {scale}"
     else:
         torch.testing.assert_close(out, ref, rtol=rtol, atol=atol)
 
@@ -35,7 +36,7 @@ def _act(x, dtype):
     return Act.from_nchw(x.to(DEV).contiguous(), dtype)
 
 
-DTYPES = [torch.float32, torch.float16]
+DTYPES = [torch.float32, torch.float16, torch.bfloat16]
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -94,10 +95,11 @@ def test_conv_epilogues(dtype):
     ]
     for kw, ref in cases:
         out = m.run(X, **kw).nchw()
-        if kw.get("act") == L.ACT_ROUND and dtype == torch.float32:
-            # rounding is exact given the same pre-activation; allow ties flipped by summation order
+        if kw.get("act") == L.ACT_ROUND and dtype != torch.float16:
+            # rounding is exact given the same pre-activation; allow values near .5 flipped by
+            # summation order (fp32) or by bf16's 8-bit operands (a few %)
             assert (out.cpu() - ref).abs().max().item() <= 1.0
-            assert (out.cpu() != ref).float().mean().item() < 1e-3
+            assert (out.cpu() != ref).float().mean().item() < (1e-3 if dtype == torch.float32 else 5e-2)
             continue
         _close(out, ref, dtype)
 

@@ -12,7 +12,8 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-DTYPES = [torch.float32, torch.float16]
+DTYPES = [torch.float32, torch.float16, torch.bfloat16]
+TOL16 = {torch.float16: 2e-2, torch.bfloat16: 4e-2}   # of the tensor scale; fp32: 1e-4
 
 
 def _rel(out, ref, dtype, name):
@@ -21,7 +22,13 @@ def _rel(out, ref, dtype, name):
     assert out.shape == ref.shape, (name, out.shape, ref.shape)
     scale = ref.abs().max().item() + 1e-12
     err = (out - ref).abs().max().item()
-    tol = 2e-2 if dtype == torch.float16 else 1e-4
+    if dtype == torch.bfloat16:
+        # 8 mantissa bits: a pre-activation within ~1e-2 of a ReLU / LeakyReLU kink can take the
+        # other branch than in fp32, so single entries of dx may differ by |dz|; bar on the norm
+        rel = ((out - ref).norm() / (ref.norm() + 1e-12)).item()
+        assert rel <= 3e-2 and err <= 0.2 * scale, f"{name}: rel norm err {rel:.3e}, max {err:.3e} vs {scale:.3e}"
+        return
+    tol = TOL16.get(dtype, 1e-4)
     assert err <= tol * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e} ({dtype})"
 
 
@@ -36,10 +43,15 @@ def _nchw(t):
 def _run(fn_gpu, fn_ref, x, params, dtype, seed=3):
     """Compare forward outputs and grads of x and params; upstream grad seeded."""
     g = torch.Generator().manual_seed(seed)
+    if dtype != torch.float32:   # the reference sees the same 16-bit-rounded activations and
+        x = x.to(dtype).float()  # packed weights (biases stay fp32 in the kernels)
+        params = [p.to(dtype).float() if p.dim() >= 2 else p for p in params]
     xr = x.clone().requires_grad_(True)
     pr = [p.clone().requires_grad_(True) for p in params]
     yr = fn_ref(xr, *pr)
     dy = torch.randn(yr.shape, generator=g)
+    if dtype != torch.float32:
+        dy = dy.to(dtype).float()
     yr.backward(dy)
 
     xg = _nhwc(x).to(DEV, dtype).requires_grad_(True)
@@ -334,8 +346,8 @@ def test_rate_train_grad(dtype):
     y = torch.randn(2, 8, 8, 48, generator=g) * 3
     mu = torch.randn(2, 8, 8, 48, generator=g)
     sc = torch.rand(2, 8, 8, 48, generator=g) * 2 - 0.2     # some scales under the 0.11 bound
-    if dtype == torch.float16:   # the reference sees the same fp16-rounded inputs
-        y, mu, sc = y.half().float(), mu.half().float(), sc.half().float()
+    if dtype != torch.float32:   # the reference sees the same 16-bit-rounded inputs
+        y, mu, sc = y.to(dtype).float(), mu.to(dtype).float(), sc.to(dtype).float()
     _check(lambda a, b, c: AG.rate_train(a, b, c, 77, 2 * 128 * 128),
            lambda a, b, c: _rate_ref(a, b, c, 77, 2 * 128 * 128), [y, mu, sc], [True] * 3, dtype)
 

@@ -15,8 +15,9 @@ Differences:
     instead of single-process ``nn.DataParallel`` (:152);
   * data: no DIV2K and no network here — ``--synthetic`` (default) draws random 256x256
     crops from a seeded bank of smooth synthetic images resident in HBM;
-  * fp16 activations (fp32 master weights, fp32 accumulation) use a dynamic loss scale
-    (torch.amp.GradScaler); ``--precision fp32`` is the parity path;
+  * ``--precision bf16`` (default, BASELINE config 5): bf16 activations / MFMA operands
+    (v_mfma_f32_32x32x16_bf16), fp32 accumulation and fp32 master weights, no loss scale;
+    ``fp16`` uses a dynamic loss scale (torch.amp.GradScaler); ``fp32`` is the parity path;
   * the NaN check (:189-190) runs every ``--log_every`` steps instead of syncing each step.
 
 ``--bench``: W warm-up + K timed steps between barriers + device syncs; rank 0 prints one
@@ -68,7 +69,8 @@ def main():
     ap.add_argument("--lambda", type=float, default=0.0025, dest="lmbda")
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--batch_size", type=float, default=8, help="images per GPU")
-    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="activation dtype (fp32 master weights, fp32 accumulation); bf16 = BASELINE config 5")
     ap.add_argument("--crop", type=int, default=256)
     ap.add_argument("--arch", default="net_unet_ha_hs", choices=["net_unet_ha_hs", "net_ga"])
     ap.add_argument("--epochs", type=int, default=1)
@@ -135,7 +137,7 @@ def main():
                 "value": round(world * B * args.steps / dt, 2), "unit": "images/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                "dtype": "f16" if args.precision == "fp16" else "f32",
+                "dtype": {"fp16": "f16", "bf16": "bf16"}.get(args.precision, "f32"),
                 "data": "synthetic (seeded smooth images, random crops in HBM; no DIV2K)",
                 "config": {"workload": f"{args.arch} Net.forward(x,'train') + backward + grad all-reduce + clip + Adam",
                            "global_batch": world * B, "crop": args.crop, "lambda": args.lmbda,
