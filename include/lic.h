@@ -426,14 +426,18 @@ int lic_avgpool_bwd(int32_t dtype, const void* dy, int32_t lddy, int32_t n, int3
  * 1e-9), s = LowerBound(scale, 0.11); partials[block] = sum ln L' (fp64,
  * lic_rate_train_parts blocks); yhat (may be NULL) = rint(y-mu)+mu (ste_round forward).
  * bwd: with gout = dLoss/dbpp (device fp32 scalar) and factor = -1/(ln2 * num_pixels):
- * dy, dmu, dscale of factor * gout * sum ln L' (LowerBound gradient rules).       */
+ * dy, dmu, dscale of factor * gout * sum ln L' (LowerBound gradient rules).
+ * seed_dev (may be NULL): the noise seed is seed_dev[0] * seed_mul + seed, read on the device,
+ * so a captured hipGraph of a training step draws a new stream per replay.        */
 int32_t lic_rate_train_parts(int32_t npix, int32_t c);
 int lic_rate_train_fwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
                        const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                       const uint64_t* seed_dev, uint64_t seed_mul,
                        float scale_bound, float likelihood_bound, void* yhat, int32_t ldyh,
                        double* partials, lic_stream_t stream);
 int lic_rate_train_bwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
                        const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                       const uint64_t* seed_dev, uint64_t seed_mul,
                        float scale_bound, float likelihood_bound, const float* gout, float factor,
                        void* dy, int32_t lddy, void* dmu, int32_t lddmu, void* dscale, int32_t lddsc,
                        lic_stream_t stream);

@@ -194,8 +194,8 @@ def load():
         "lic_half_tanh_fwd": [I, V, I, V, I, I, I, V, I, V],
         "lic_half_tanh_bwd": [I, V, I, V, I, I, I, V, I, V],
         "lic_avgpool_bwd": [I, V, I, I, I, I, V, I, V],
-        "lic_rate_train_fwd": [I, V, I, V, I, V, I, I, I, U, F, F, V, I, V, V],
-        "lic_rate_train_bwd": [I, V, I, V, I, V, I, I, I, U, F, F, V, F, V, I, V, I, V, I, V],
+        "lic_rate_train_fwd": [I, V, I, V, I, V, I, I, I, U, V, U, F, F, V, I, V, V],
+        "lic_rate_train_bwd": [I, V, I, V, I, V, I, I, I, U, V, U, F, F, V, F, V, I, V, I, V, I, V],
         "lic_recon_train_fwd": [I, V, I, I, I, I, V, I, V, V, V, V],
         "lic_recon_train_bwd": [I, V, I, I, I, I, V, I, V, V, F, V, I, V, V, L, V],
         "lic_dwconv_wgrad": [I, V, I, V, I, I, I, I, I, I, I, I, I, V, V, V, V, L, V],

@@ -559,14 +559,15 @@ def win_attn(qkv: torch.Tensor, table: torch.Tensor, C: int, heads: int, ws: int
 class _RateTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, mu, sc, cfg):
-        seed, num_pixels, sb, lb = cfg
+        seed, num_pixels, sb, lb, sdev, smul = cfg
         y, mu, sc = y.contiguous(), mu.contiguous(), sc.contiguous()
         C = y.shape[-1]
         npix = _npix(y)
         nparts = int(_lib().lic_rate_train_parts(npix, C))
         parts = torch.empty((max(nparts, 1),), dtype=torch.float64, device=y.device)
         yhat = torch.empty_like(y)
-        check(_lib().lic_rate_train_fwd(dtype_id(y.dtype), _dp(y), C, _dp(mu), C, _dp(sc), C, npix, C, seed, sb, lb,
+        check(_lib().lic_rate_train_fwd(dtype_id(y.dtype), _dp(y), C, _dp(mu), C, _dp(sc), C, npix, C, seed,
+                                        _dp(sdev) if sdev is not None else None, smul, sb, lb,
                                         _dp(yhat), C, _dp(parts), stream_handle()))
         bpp = torch.empty((), dtype=torch.float32, device=y.device)
         Fn.bpp_finalize(parts, nparts, num_pixels, bpp)
@@ -577,14 +578,15 @@ class _RateTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gb, gy):
         y, mu, sc = ctx.saved_tensors
-        seed, num_pixels, sb, lb = ctx.cfg
+        seed, num_pixels, sb, lb, sdev, smul = ctx.cfg
         C = y.shape[-1]
         npix = _npix(y)
         if gb is None:
             gb = torch.zeros((), dtype=torch.float32, device=y.device)
         gout = gb.detach().float().reshape(1).contiguous()
         dy, dmu, dsc = torch.empty_like(y), torch.empty_like(mu), torch.empty_like(sc)
-        check(_lib().lic_rate_train_bwd(dtype_id(y.dtype), _dp(y), C, _dp(mu), C, _dp(sc), C, npix, C, seed, sb, lb,
+        check(_lib().lic_rate_train_bwd(dtype_id(y.dtype), _dp(y), C, _dp(mu), C, _dp(sc), C, npix, C, seed,
+                                        _dp(sdev) if sdev is not None else None, smul, sb, lb,
                                         _dp(gout), -1.0 / (math.log(2.0) * num_pixels), _dp(dy), C, _dp(dmu), C,
                                         _dp(dsc), C, stream_handle()))
         if gy is not None:   # ste_round(y - mu) + mu: d/dy = 1, d/dmu = 0
@@ -593,11 +595,16 @@ class _RateTrainFn(torch.autograd.Function):
 
 
 def rate_train(y: torch.Tensor, mu: torch.Tensor, scale: torch.Tensor, seed: int, num_pixels: float,
-               scale_bound: float = 0.11, likelihood_bound: float = 1e-9):
+               scale_bound: float = 0.11, likelihood_bound: float = 1e-9, seed_dev: Optional[torch.Tensor] = None,
+               seed_mul: int = 0):
     """Training-mode GaussianConditional of one slice (net_ga.py:1049 with noise) -> (bpp contribution
-    sum ln L / (-ln 2 * num_pixels) as a 0-d fp32 tensor, ste_round(y - mu) + mu)."""
+    sum ln L / (-ln 2 * num_pixels) as a 0-d fp32 tensor, ste_round(y - mu) + mu).  With seed_dev (a
+    1-element int64 device tensor) the noise seed is seed_dev * seed_mul + seed, read by the kernels,
+    so a captured training step draws a fresh stream on every replay."""
+    if seed_dev is not None and (seed_dev.dtype != torch.int64 or not seed_dev.is_cuda):
+        raise ValueError("rate_train: seed_dev must be an int64 device tensor")
     return _RateTrainFn.apply(y, mu, scale, (int(seed) & (2 ** 64 - 1), float(num_pixels), float(scale_bound),
-                                             float(likelihood_bound)))
+                                             float(likelihood_bound), seed_dev, int(seed_mul)))
 
 
 class _ReconMSEFn(torch.autograd.Function):

@@ -6,6 +6,10 @@
 #ifndef HALO_BIG_TILE
 #define HALO_BIG_TILE 1
 #endif
+// 1x1 convolutions (GEMMs) on the halo kernel: 1 = fp32, 2 = fp32 and 16-bit, 0 = never
+#ifndef HALO_1X1
+#define HALO_1X1 1
+#endif
 
 namespace lic {
 
@@ -24,7 +28,8 @@ int try_halo(const lic_conv_args& a, hipStream_t s, int& status);
 // (the 16x16 latents of the slice loop).
 template <typename T>
 static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
-  if (a.groups != 1 || a.ntaps < 2 || a.prologue != LIC_PRO_NONE || a.force_direct) return 0;
+  const bool gemm_ok = a.ntaps == 1 && (HALO_1X1 == 2 || (HALO_1X1 == 1 && sizeof(T) == 4));
+  if (a.groups != 1 || (a.ntaps < 2 && !gemm_ok) || a.prologue != LIC_PRO_NONE || a.force_direct) return 0;
   auto blocks = [&](int th, int tw, int bn) {
     return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
   };

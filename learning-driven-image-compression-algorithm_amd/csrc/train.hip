@@ -59,17 +59,35 @@ __global__ __launch_bounds__(WM * WN * 64) void wgrad_kernel(const lic_wgrad_arg
   const int row0 = cg * EPC;
 
   u32x4 v[EPC];
-  auto gload = [&](int k0) {
+  // Running (image, row, col) of this thread's first pixel of the next K step: decoded once
+  // with divisions, then advanced by BK pixels per step and by one pixel per element with
+  // carries (the per-element divisions made the kernel VALU-bound, ~8x the MFMA time).
+  int cur_k = kbeg + pg * EPC, cur_b, cur_i, cur_j;
+  {
+    cur_b = cur_k / mij;
+    const int rem = cur_k - cur_b * mij;
+    cur_i = rem / a.mj;
+    cur_j = rem - cur_i * a.mj;
+  }
+  auto step_pix = [&](int& b, int& i, int& j, int d) {
+    j += d;
+    while (j >= a.mj) {
+      j -= a.mj;
+      if (++i == a.mi) {
+        i = 0;
+        ++b;
+      }
+    }
+  };
+  auto gload = [&](int /*k0*/) {
+    int b = cur_b, i = cur_i, j = cur_j;
 #pragma unroll
     for (int e = 0; e < EPC; ++e) {
-      const int k = k0 + pg * EPC + e;
+      const int k = cur_k + e;
+      if (e) step_pix(b, i, j, 1);
       bool ok = ch_ok && k < kend;
       int64_t off = 0;
       if (ok) {
-        const int b = k / mij;
-        const int rem = k - b * mij;
-        const int i = rem / a.mj;
-        const int j = rem - i * a.mj;
         if (isA) {
           const int oy = a.oy0 + a.osy * i, ox = a.ox0 + a.osx * j;
           off = ((int64_t)(b * a.ho + oy) * a.wo + ox) * a.ldz + ch;
@@ -83,6 +101,8 @@ __global__ __launch_bounds__(WM * WN * 64) void wgrad_kernel(const lic_wgrad_arg
       if (!ok) r = u32x4{0u, 0u, 0u, 0u};
       v[e] = r;
     }
+    cur_k += BK;
+    step_pix(cur_b, cur_i, cur_j, BK);
   };
 
   auto sstore = [&](int buf) {
@@ -696,9 +716,11 @@ __device__ __forceinline__ float noise_u(uint64_t seed, uint64_t i) {
 template <typename T>
 __global__ __launch_bounds__(256) void rate_train_fwd_kernel(const T* __restrict__ y, int ldy, const T* __restrict__ mu,
                                                              int ldmu, const T* __restrict__ sc, int ldsc, int npix,
-                                                             int c, uint64_t seed, float sbound, float lbound,
+                                                             int c, uint64_t seed, const uint64_t* seed_dev,
+                                                             uint64_t seed_mul, float sbound, float lbound,
                                                              T* __restrict__ yhat, int ldyh, double* __restrict__ parts) {
   __shared__ double red[4];
+  if (seed_dev) seed = seed_dev[0] * seed_mul + seed;   // graph replays: the step's seed lives on the device
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   double acc = 0.0;
   if (idx < (int64_t)npix * c) {
@@ -720,9 +742,11 @@ __global__ __launch_bounds__(256) void rate_train_fwd_kernel(const T* __restrict
 template <typename T>
 __global__ void rate_train_bwd_kernel(const T* __restrict__ y, int ldy, const T* __restrict__ mu, int ldmu,
                                       const T* __restrict__ sc, int ldsc, int npix, int c, uint64_t seed,
+                                      const uint64_t* seed_dev, uint64_t seed_mul,
                                       float sbound, float lbound, const float* __restrict__ gout, float factor,
                                       T* __restrict__ dy, int lddy, T* __restrict__ dmu, int lddmu,
                                       T* __restrict__ dsc, int lddsc) {
+  if (seed_dev) seed = seed_dev[0] * seed_mul + seed;   // graph replays: the step's seed lives on the device
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (int64_t)npix * c) return;
   const int64_t p = idx / c;
@@ -1121,6 +1145,7 @@ extern "C" int32_t lic_rate_train_parts(int32_t npix, int32_t c) { return (int32
 
 extern "C" int lic_rate_train_fwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
                                   const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                                  const uint64_t* seed_dev, uint64_t seed_mul,
                                   float scale_bound, float likelihood_bound, void* yhat, int32_t ldyh,
                                   double* partials, lic_stream_t stream) {
   const int64_t total = (int64_t)npix * c;
@@ -1128,13 +1153,14 @@ extern "C" int lic_rate_train_fwd(int32_t dtype, const void* y, int32_t ldy, con
   TR_DISPATCH(dtype, "rate_train_fwd",
               hipLaunchKernelGGL(rate_train_fwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
                                  (const T*)y, ldy, (const T*)mu, ldmu, (const T*)scale, ldsc, npix, c, seed,
-                                 scale_bound, likelihood_bound, (T*)yhat, ldyh, partials));
+                                 seed_dev, seed_mul, scale_bound, likelihood_bound, (T*)yhat, ldyh, partials));
   LIC_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int lic_rate_train_bwd(int32_t dtype, const void* y, int32_t ldy, const void* mu, int32_t ldmu,
                                   const void* scale, int32_t ldsc, int32_t npix, int32_t c, uint64_t seed,
+                                  const uint64_t* seed_dev, uint64_t seed_mul,
                                   float scale_bound, float likelihood_bound, const float* gout, float factor,
                                   void* dy, int32_t lddy, void* dmu, int32_t lddmu, void* dscale, int32_t lddsc,
                                   lic_stream_t stream) {
@@ -1143,7 +1169,7 @@ extern "C" int lic_rate_train_bwd(int32_t dtype, const void* y, int32_t ldy, con
   TR_DISPATCH(dtype, "rate_train_bwd",
               hipLaunchKernelGGL(rate_train_bwd_kernel<T>, dim3(tr_nblk(total)), dim3(256), 0, (hipStream_t)stream,
                                  (const T*)y, ldy, (const T*)mu, ldmu, (const T*)scale, ldsc, npix, c, seed,
-                                 scale_bound, likelihood_bound, gout, factor, (T*)dy, lddy, (T*)dmu, lddmu,
+                                 seed_dev, seed_mul, scale_bound, likelihood_bound, gout, factor, (T*)dy, lddy, (T*)dmu, lddmu,
                                  (T*)dscale, lddsc));
   LIC_CHECK_LAUNCH();
   return 0;

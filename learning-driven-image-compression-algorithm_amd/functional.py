@@ -447,7 +447,7 @@ def rate_noise(y: Act, mu: Act, scale: Act, seed: int, partials: torch.Tensor, p
     if part_off + n > partials.numel():
         raise ValueError("rate_noise: partials buffer too small")
     check(_lib().lic_rate_train_fwd(dtype_id(y.dtype), y.ptr, y.ld, mu.ptr, mu.ld, scale.ptr, scale.ld, y.npix, y.c,
-                                    int(seed) & 0xFFFFFFFFFFFFFFFF, scale_bound, likelihood_bound, None, 0,
+                                    int(seed) & 0xFFFFFFFFFFFFFFFF, None, 0, scale_bound, likelihood_bound, None, 0,
                                     _dp(partials) + part_off * 8, stream_handle()))
     return n
 

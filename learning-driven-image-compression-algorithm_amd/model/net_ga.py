@@ -733,7 +733,8 @@ class Net(nn.Module):
 
     # ---- forward
     def forward(self, inputs: torch.Tensor, mode: str = 'train', num: int = 1, return_intermediates: bool = False,
-                seed: Optional[int] = None, noise_seed: Optional[int] = None):
+                seed: Optional[int] = None, noise_seed: Optional[int] = None,
+                seed_dev: Optional[torch.Tensor] = None):
         """mode='test': (bpp, v_mse, v_psnr) (no autograd).  The rate uses eval ('dequantize')
         semantics unless ``noise_seed`` is given: then it prices y + U(-1/2, 1/2) from that seed,
         as the reference's eval does (its nets stay in training mode, net_ga.py:1049,
@@ -741,7 +742,8 @@ class Net(nn.Module):
         value is reproducible; symbols / y_hat / x_rec do not depend on it).
         mode='train': (bpp, mse) differentiable through liblic (lic_amd/train_net.py); ``seed``
         picks the GaussianConditional noise stream (default: a per-module counter); the same
-        seed gives the same noise as ``noise_seed`` in 'test'."""
+        seed gives the same noise as ``noise_seed`` in 'test'.  ``seed_dev`` (int64 device scalar)
+        replaces ``seed`` by a device-resident value (hipGraph-captured training steps)."""
         if not inputs.is_cuda:
             raise RuntimeError("lic_amd Net runs on the GPU only (HIP path); move inputs to cuda")
         if mode == 'train':
@@ -749,7 +751,7 @@ class Net(nn.Module):
             if seed is None:
                 seed = self.__dict__.get("_train_calls", 0)
                 self.__dict__["_train_calls"] = seed + 1
-            return net_forward_train(self, inputs, seed)
+            return net_forward_train(self, inputs, seed, seed_dev)
         if mode != 'test':
             raise ValueError(f"mode must be 'train' or 'test', got {mode!r}")
         with torch.no_grad():

@@ -308,7 +308,7 @@ def _cc(seq, x):
     return conv(seq[4], conv(seq[2], conv(seq[0], x, ACT_GELU), ACT_GELU))
 
 
-def net_forward_train(net, inputs: torch.Tensor, seed: int) -> Tuple[torch.Tensor, torch.Tensor]:
+def net_forward_train(net, inputs: torch.Tensor, seed: int, seed_dev=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """net_ga.Net.forward(inputs, 'train') -> (bpp, mse), differentiable through liblic
     (net_unet_ha_hs.Net: the U-Net hyper nets of net_unet_ha_hs.py:880-895)."""
     if net.arch not in ("net_ga", "net_unet_ha_hs"):
@@ -350,8 +350,12 @@ def net_forward_train(net, inputs: torch.Tensor, seed: int) -> Tuple[torch.Tenso
         ss = swatten(net.atten_scale[i][0], torch.cat([latent_scales] + support, -1))
         sc = _cc(net.cc_scale_transforms[i], ss)
         y_i = z3[..., sw * i:sw * (i + 1)].contiguous()
-        b_i, yq = AG.rate_train(y_i, mu, sc, seed * net.num_slices + i, num_pixels, gc._scale_bound,
-                                gc._likelihood_bound)
+        if seed_dev is None:
+            b_i, yq = AG.rate_train(y_i, mu, sc, seed * net.num_slices + i, num_pixels, gc._scale_bound,
+                                    gc._likelihood_bound)
+        else:   # captured step: the kernels read the step's seed from the device
+            b_i, yq = AG.rate_train(y_i, mu, sc, i, num_pixels, gc._scale_bound, gc._likelihood_bound,
+                                    seed_dev=seed_dev, seed_mul=net.num_slices)
         bpp = b_i if bpp is None else bpp + b_i
         lrp = _cc(net.lrp_transforms[i], torch.cat([ms, yq], -1))
         y_hats.append(AG.half_tanh_add(lrp, yq))                      # y_hat + 0.5 tanh(lrp)

@@ -273,3 +273,65 @@ def test_net_train_step_bf16(arch):
     assert abs(bpp.item() - bpp_r.item()) <= 2e-2 * abs(bpp_r.item())
     assert abs(mse.item() - mse_r.item()) <= 2e-2 * abs(mse_r.item())
     assert len(cos) > 300 and cos[len(cos) // 10] >= 0.98 and cos[len(cos) // 2] >= 0.995
+
+
+def test_train_step_hipgraph_matches_eager():
+    """train_net_unet.py --graph: the whole step (forward, backward, clip_grad_norm_, capturable
+    Adam) captured once and replayed, with the noise seed on the device (lic_rate_train_* seed_dev),
+    gives the same parameters as the same steps run eagerly (same kernels, same order)."""
+    import copy
+    from lic_amd.model import net_unet_ha_hs, net_ga
+    torch.manual_seed(0)
+    base = net_ga.synthetic_syntax_bias_(net_unet_ha_hs.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False,
+                                                            precision="bf16"))
+    x = (torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(9)) * 2 - 1).to(DEV)
+    lmbda, steps = 0.0025, 3
+
+    def make():
+        net = copy.deepcopy(base).to(DEV)
+        params = net.base_params()
+        opt = torch.optim.Adam(params, lr=torch.tensor(1e-4, device=DEV), capturable=True)
+        return net, params, opt, torch.zeros((1,), dtype=torch.int64, device=DEV)
+
+    def body(net, params, opt, seed_t):
+        bpp, mse = net(x, "train", seed_dev=seed_t)
+        loss = lmbda * 255 ** 2 * mse + bpp
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_([p for p in params if p.grad is not None], 1.0)
+        opt.step()
+        seed_t.add_(1)
+        return loss.detach()
+
+    def eager():
+        net_a, pa, oa, sa = make()
+        losses = []
+        for _ in range(steps):
+            oa.zero_grad(set_to_none=True)
+            losses.append(body(net_a, pa, oa, sa).item())
+        return net_a, losses
+
+    net_a, losses_a = eager()
+    _, losses_a2 = eager()
+    net_b, pb, ob, sb = make()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ob.zero_grad(set_to_none=True)
+        first = body(net_b, pb, ob, sb).item()               # eager warm-up = step 1
+    torch.cuda.current_stream().wait_stream(side)
+    ob.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):   # the warm-up's stream: AccumulateGrad nodes stay on it
+        out = body(net_b, pb, ob, sb)
+    losses_b = [first]
+    for _ in range(steps - 1):
+        g.replay()
+        losses_b.append(out.item())
+    torch.cuda.synchronize()
+    print(f"\n[train hipGraph] eager losses {losses_a} / {losses_a2}, graph losses {losses_b}")
+    assert int(sb.item()) == steps
+    for la, lb in zip(losses_a, losses_b):
+        assert abs(la - lb) <= 1e-4 * abs(la)
+    d = max(((p - q).norm() / (p.norm() + 1e-12)).item() for p, q in zip(net_a.parameters(), net_b.parameters()))
+    print(f"[train hipGraph] max relative parameter difference {d:.2e}")
+    assert d <= 1e-4

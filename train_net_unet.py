@@ -80,6 +80,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gpus", type=int, default=1, help="informational; world size comes from torchrun")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole step (forward, backward, clip, Adam) in one hipGraph and replay it: "
+                         "no per-launch host cost; the noise seed lives on the device (bf16 / fp32, one GPU)")
     args = ap.parse_args()
 
     from lic_amd import distributed as D
@@ -97,13 +100,58 @@ def main():
         net.load_state_dict(torch.load(args.weight_path, map_location="cpu", weights_only=True), strict=True)
     net = net.to(dev)
     params = net.base_params()
-    opt = torch.optim.Adam(params, lr=args.lr)
+    if args.graph and (args.precision == "fp16" or world > 1):
+        raise SystemExit("--graph: bf16 / fp32 on one GPU (GradScaler syncs the host; the grad all-reduce is "
+                         "not captured)")
+    # capturable Adam keeps lr and the step count on the device (graph replays update them)
+    opt = torch.optim.Adam(params, lr=torch.tensor(args.lr, device=dev) if args.graph else args.lr,
+                           capturable=args.graph)
     sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1500, 2500, 3500, 4000], 0.5)
     sync = D.GradAllReduce(params, world)
     scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 10, enabled=args.precision == "fp16")
     batches = Crops(synthetic_bank(16, 2 * args.crop, 5000 + 97 * rank, dev), B, args.crop, 1234 + rank)
 
-    def step():
+    grad_params = None
+
+    def step_body(x, seed_dev=None):
+        bpp, mse = net(x, "train", seed_dev=seed_dev)
+        loss = args.lmbda * 255 ** 2 * mse + bpp                       # :180
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(grad_params, 1.0)               # :198
+        opt.step()
+        return loss.detach(), bpp.detach(), mse.detach()
+
+    if args.graph:
+        # W eager warm-up steps (Adam state, caches) on a side stream, then one capture
+        static_x = batches().clone()
+        seed_t = torch.zeros((1,), dtype=torch.int64, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, args.warmup)):
+                opt.zero_grad(set_to_none=True)
+                bpp, mse = net(static_x, "train", seed_dev=seed_t)
+                (args.lmbda * 255 ** 2 * mse + bpp).backward()
+                grad_params = [p for p in params if p.grad is not None]
+                torch.nn.utils.clip_grad_norm_(grad_params, 1.0)
+                opt.step()
+                seed_t.add_(1)
+        torch.cuda.current_stream().wait_stream(side)
+        opt.zero_grad(set_to_none=True)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=side):   # the warm-up's stream: AccumulateGrad nodes stay on it
+            outs = step_body(static_x, seed_t)
+            seed_t.add_(1)
+
+        def step():
+            static_x.copy_(batches())
+            graph.replay()
+            return outs
+    else:
+        def step():
+            return eager_step()
+
+    def eager_step():
         x = batches()
         opt.zero_grad(set_to_none=True)
         bpp, mse = net(x, "train")
