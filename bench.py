@@ -43,7 +43,8 @@ def _env_int(k, d):
 
 
 PMC_FILES = {torch.float16: "profiles/r02/pmc_conv3x3_64_f16.json",
-             torch.float32: "profiles/r02/pmc_conv3x3_64_f32.json"}
+             torch.float32: "profiles/r02/pmc_conv3x3_64_f32.json",
+             "split": "profiles/r02/pmc_conv3x3_64_f32x3.json"}
 
 
 def _pmc_file(dtype):
@@ -94,9 +95,16 @@ def time_graph(g, iters):
     return (time.perf_counter() - t0) / iters
 
 
-def dominant_kernel_roofline(dtype, batch, device, iters=30):
+def dominant_kernel_roofline(dtype, batch, device, iters=30, split=False):
     """conv3x3 192->192 s1 at 64x64 (Win_noShift_Attention @ H/4 of a 256 image): avg launch
     duration from HIP events recorded on the launch stream."""
+    from lic_amd.layers import Conv2d
+    from lic_amd.functional import Act, split_f32
+    with split_f32(split):
+        return _dominant(dtype, batch, device, iters)
+
+
+def _dominant(dtype, batch, device, iters):
     from lic_amd.layers import Conv2d
     from lic_amd.functional import Act
     torch.manual_seed(1)
@@ -183,9 +191,10 @@ def forward_rate(net, x, iters=10):
 
 
 def a_model_rate(net, x, dtype, iters=10):
-    from lic_amd.functional import Act
+    from lic_amd.functional import Act, split_f32
     xin = Act(x.to(dtype).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1))
-    ga, _ = capture(lambda: net.a_model.run(xin))
+    with split_f32(net.precision == "fp32x3"):
+        ga, _ = capture(lambda: net.a_model.run(xin))
     return time_graph(ga, iters)
 
 
@@ -197,7 +206,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--arch", default="net_ga", choices=["net_ga", "net_unet_ha_hs"])
-    ap.add_argument("--precision", default="fp32", choices=["fp16", "fp32"],
+    ap.add_argument("--precision", default="fp32", choices=["fp16", "fp32", "fp32x3"],
                     help="fp32 = the reference's precision (parity grade, the headline); fp16 activations are "
                          "reported as an extra and do not meet the symbol / bpp bar")
     ap.add_argument("--no-extras", action="store_true", help="skip cpu baseline / parity / fp16 legs")
@@ -250,13 +259,15 @@ def main():
             print(json.dumps({"profile_run": True, "value": round(value, 2), "ms_per_step": round(ms_per_step, 3)}))
         return
     if rank == 0:
-        peak = FP16_PEAK_TFLOPS if dtype == torch.float16 else FP32_PEAK_TFLOPS
-        flops, tk = dominant_kernel_roofline(dtype, args.batch, device)
+        split = args.precision == "fp32x3"
+        # fp32x3: three fp16 MFMA products per algorithmic one -> its ceiling is 1/3 of the fp16 peak
+        peak = FP16_PEAK_TFLOPS if dtype == torch.float16 else (FP16_PEAK_TFLOPS / 3 if split else FP32_PEAK_TFLOPS)
+        flops, tk = dominant_kernel_roofline(dtype, args.batch, device, split=split)
         achieved = flops / tk / 1e12
         ta = a_model_rate(net, x, dtype)
         gf_a = A_MODEL_GFLOP_256 * (args.size / 256) ** 2
         a_tflops = gf_a * args.batch / ta / 1e3
-        dname = "f16" if dtype == torch.float16 else "f32"
+        dname = "f16" if dtype == torch.float16 else ("f32 (fp16x3 split products)" if split else "f32")
         result = {
             "metric": f"images/sec encode+decode ({args.size}x{args.size})",
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
@@ -270,13 +281,15 @@ def main():
                        "global_batch": args.batch * world, "image_size": args.size,
                        "parallelism": f"image-sharded x{world} (independent batches, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": _pmc_traffic(dtype, args.batch, args.size),
+                         "frac": round(achieved / peak, 4), "traffic": _pmc_traffic("split" if split else dtype, args.batch, args.size),
                          "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} (conv_halo_kernel {dname}), "
                                    f"{flops / 1e9:.1f} GFLOP/launch, {tk * 1e6:.1f} us/launch",
-                         "peak_note": ("fp32-input MFMA v_mfma_f32_32x32x2_f32 (exact fp32, 1/16 of the fp16 rate)"
+                         "peak_note": ("fp16 dense MFMA / 3 (each fp32 product = 3 fp16 MFMA products, "
+                                       "csrc/conv_halo_split.hip)" if split else
+                                       "fp32-input MFMA v_mfma_f32_32x32x2_f32 (exact fp32, 1/16 of the fp16 rate)"
                                        if dtype == torch.float32 else "fp16 dense MFMA"),
                          "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
-                                         "separate --pmc passes: " + _pmc_file(dtype)},
+                                         "separate --pmc passes: " + _pmc_file("split" if split else dtype)},
             "a_model": {"ms": round(ta * 1e3, 3), "images_per_s": round(args.batch / ta, 2),
                         "tflops": round(a_tflops, 2), "frac_of_peak": round(a_tflops / peak, 4),
                         "gflop_per_image": gf_a},
@@ -289,7 +302,7 @@ def main():
             result["cfg2_a_model"] = {"gpu_images_per_s": result["a_model"]["images_per_s"], "dtype": dname,
                                       "cpu_baseline": cpu_baseline(args.arch, args.size, n_img=16, reps=5,
                                                                    what="a_model")}
-            other = "fp16" if args.precision == "fp32" else "fp32"
+            other = "fp16" if args.precision != "fp16" else "fp32"
             odt = torch.float16 if other == "fp16" else torch.float32
             net2 = build_net(args.arch, other, args.size, args.batch, "cpu", seed=0).to(device)
             t2 = forward_rate(net2, x)

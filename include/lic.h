@@ -84,6 +84,12 @@ typedef struct lic_conv_args {
   int32_t out_shuffle;               /* 0, 2 or 3 */
   int32_t force_direct;              /* testing: force the non-MFMA kernel */
   int32_t force_mfma_generic;        /* testing: skip the spatial-tile (halo) kernel */
+  /* fp32 only: 1 = form the products on the fp16 matrix cores from fp16 parts (x_hi*W1 +
+   * x_hi*W2 + x_lo*W1, x_lo = fp16(x - fp16(x)), ~3e-7 relative per product) where a spatial-tile config applies, with
+   * wgt_split = the same weights packed [copad][ntaps][cpad/16][W1 16 | W2 16] in fp16,
+   * W1 = fp16(w)*2^11, W2 = fp16((w - fp16(w))*2^11); other launches use wgt (exact fp32). */
+  int32_t mfma_mode;
+  const void* wgt_split;
 } lic_conv_args;
 
 /* Convolution / linear layer (nn.Conv2d, nn.ConvTranspose2d phase, nn.Linear as

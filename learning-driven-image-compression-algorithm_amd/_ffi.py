@@ -65,6 +65,8 @@ class ConvArgs(ctypes.Structure):
         ("out_shuffle", _i32),
         ("force_direct", _i32),
         ("force_mfma_generic", _i32),
+        ("mfma_mode", _i32),
+        ("wgt_split", _vp),
     ]
 
 

@@ -358,7 +358,9 @@ _IGNORED_PREFIXES = ("y_sampler.", "h_sampler.", "test_y_sampler.", "test_h_samp
 
 class Net(nn.Module):
     """net_ga.Net (net_ga.py:735-1144).  ``precision`` selects the activation dtype of
-    the HIP path: 'fp32' (parity), 'fp16' or 'bf16' (fp32 accumulation; bf16 is the training
+    the HIP path: 'fp32' (parity, exact-fp32 MFMA), 'fp32x3' (fp32 activations whose spatial-tile
+    convolutions form each product from fp16 parts on the fp16 matrix cores, ~3e-7 relative;
+    csrc/conv_halo_split.hip), 'fp16' or 'bf16' (fp32 accumulation; bf16 is the training
     precision of BASELINE config 5)."""
 
     arch = "net_ga"
@@ -373,8 +375,8 @@ class Net(nn.Module):
         self.test_size = test_size
         self.post_processing = post_processing
         self.is_high = is_high
-        if precision not in ("fp32", "fp16", "bf16"):
-            raise ValueError(f"precision must be 'fp32', 'fp16' or 'bf16', got {precision!r}")
+        if precision not in ("fp32", "fp32x3", "fp16", "bf16"):
+            raise ValueError(f"precision must be 'fp32', 'fp32x3', 'fp16' or 'bf16', got {precision!r}")
         self.precision = precision
         N, M = (384, 32) if is_high else (192, 16)
         self.M, self.N = M, N
@@ -599,8 +601,11 @@ class Net(nn.Module):
         self.update()
         return self.__dict__["_coder"][1]
 
-    @torch.no_grad()
     def compress(self, inputs: torch.Tensor):
+        with torch.no_grad(), Fn.split_f32(self.precision == "fp32x3"):
+            return self._compress(inputs)
+
+    def _compress(self, inputs: torch.Tensor):
         """Encode a batch to bitstreams: {"strings": [y_strings, z_strings], "shape": z's (h, w),
         "syntax": int32 [B, M]} (one bytes string per image in each list)."""
         from .. import entropy_coder as EC
@@ -630,8 +635,11 @@ class Net(nn.Module):
         return {"strings": [EC.to_strings(ywords, yoff, B, 192), EC.to_strings(zwords, zoff, B, z.c)],
                 "shape": (z.H, z.W), "syntax": syntax.cpu(), "symbols": SYM}
 
-    @torch.no_grad()
     def decompress(self, strings, shape, syntax: torch.Tensor, device="cuda"):
+        with torch.no_grad(), Fn.split_f32(self.precision == "fp32x3"):
+            return self._decompress(strings, shape, syntax, device)
+
+    def _decompress(self, strings, shape, syntax: torch.Tensor, device="cuda"):
         """Decode bitstreams from compress() -> {"x_hat": [B, 3, H, W] fp32 in [-1, 1],
         "symbols": int32 [B, h, w, 192]}; raises on a corrupt stream."""
         from .. import entropy_coder as EC
@@ -754,7 +762,7 @@ class Net(nn.Module):
             return net_forward_train(self, inputs, seed, seed_dev)
         if mode != 'test':
             raise ValueError(f"mode must be 'train' or 'test', got {mode!r}")
-        with torch.no_grad():
+        with torch.no_grad(), Fn.split_f32(self.precision == "fp32x3"):
             return self._forward_test(inputs, return_intermediates, noise_seed)
 
     def _forward_test(self, inputs: torch.Tensor, return_intermediates: bool, noise_seed: Optional[int] = None):

@@ -1,0 +1,79 @@
+"""precision='fp32x3': fp32 activations whose spatial-tile convolutions form every product
+from fp16 parts on the fp16 matrix cores (csrc/conv_halo_split.hip; include/lic.h mfma_mode):
+2^11 x w ~= x_hi*W1 + x_hi*W2 + x_lo*W1 (x_hi = fp16(x), x_lo = fp16(x - x_hi)), ~3e-7 relative per product (fp32: 6e-8).
+
+Bars: per kernel, max error <= 3e-6 of the output scale against torch fp32 on the CPU and
+<= 5e-6 against the exact-fp32 MFMA kernel on the same pack (both sides carry rounding error); end to end, the fp32 parity bars
+(bpp 1e-5, PSNR 1e-4 dB, symbols by tests/parity.py, decoder pinned)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_cpu as R
+from parity import check_decoder, check_symbols
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("cin,cout,k,s,pad,B,H,epi", [
+    (192, 192, 3, 1, (1, 1, 1, 1), 8, 64, "plain"),    # WNSA conv3x3 (16x16 x 192 tiles)
+    (192, 192, 7, 1, (3, 3, 3, 3), 8, 64, "lrelu_r1"),  # conv7x7, tap groups
+    (192, 192, 5, 2, (1, 1, 2, 2), 4, 128, "plain"),   # ZeroPad2d((1,2,1,2)) + conv5x5 s2
+    (192, 192, 3, 1, (1, 1, 1, 1), 32, 16, "gelu"),    # slice-loop latents (8x8 x 64 tiles)
+    (128, 64, 3, 1, (1, 1, 1, 1), 32, 16, "gate"),     # 8x8 tiles, 64-wide blocks, gate epilogue
+    (96, 128, 3, 1, (1, 1, 1, 1), 8, 50, "plain"),     # ragged map, 16x16 x 64 tiles
+])
+def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi):
+    import lic_amd.functional as Fn
+    from lic_amd import _ffi as L
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(41 + k + H)
+    m = Conv2d(cin, cout, k, s, 0).to(DEV)
+    with torch.no_grad():
+        m.bias.normal_(0, 0.1)
+    x = torch.randn(B, cin, H, H) * 0.5
+    X = Fn.Act.from_nchw(x.to(DEV).contiguous(), torch.float32)
+    pk = m.packed(torch.float32, pad)
+    Ho, Wo = Fn.conv_out_hw(H, H, pk)
+    r = Fn.Act.from_nchw(torch.randn(B, cout, Ho, Wo).to(DEV), torch.float32)
+    g = Fn.Act.from_nchw(torch.rand(B, cout, Ho, Wo).to(DEV), torch.float32)
+    kw = {"plain": {}, "gelu": dict(act=L.ACT_GELU), "lrelu_r1": dict(act=L.ACT_LRELU, r1=r),
+          "gate": dict(act=L.ACT_LRELU, epi=L.EPI_GATE, g=g, r2=r, r1=r)}[epi]
+    exact = Fn.conv(X, pk, **kw).nchw().cpu()
+    with Fn.split_f32(True):
+        got = Fn.conv(X, pk, **kw).nchw().cpu()
+    assert Fn.split_weights(pk) is not None
+    scale = exact.abs().max().item()
+    err = (got - exact).abs().max().item()
+    base = F.conv2d(F.pad(x, (pad[1], pad[3], pad[0], pad[2])), m.weight.detach().cpu(), m.bias.detach().cpu(), s)
+    err_cpu = (got - {"plain": base, "gelu": F.gelu(base), "lrelu_r1": None, "gate": None}[epi]).abs().max().item() \
+        if epi in ("plain", "gelu") else 0.0
+    print(f"\n[split conv{k}x{k} {cin}->{cout} B={B} {H}^2 {epi}] max err vs exact-fp32 kernel {err:.2e}, "
+          f"vs torch {err_cpu:.2e} (scale {scale:.2f})")
+    assert not torch.equal(got, exact)          # the split kernel ran
+    assert err <= 5e-6 * scale and err_cpu <= 3e-6 * scale
+
+
+def _net(arch, B=1, S=256, seed=0):
+    from lic_amd.model import net_ga, net_unet_ha_hs
+    torch.manual_seed(seed)
+    mod = net_ga if arch == "net_ga" else net_unet_ha_hs
+    return net_ga.synthetic_syntax_bias_(mod.Net((B, S, S, 3), (B, S, S, 3), False, False, precision="fp32x3"), seed)
+
+
+@pytest.mark.parametrize("arch,B", [("net_ga", 1), ("net_unet_ha_hs", 1), ("net_ga", 32)])
+def test_fp32x3_net_parity(arch, B):
+    net = _net(arch, B)
+    P = {k: v.detach().float() for k, v in net.state_dict().items()}
+    net = net.to(DEV)
+    x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(123 + B)) * 2 - 1
+    bpp, v_mse, v_psnr = net(x.to(DEV), "test", return_intermediates=True)
+    torch.cuda.synchronize()
+    ref = R.net_forward(x, P, arch=arch)
+    flips = check_symbols(net.last["symbols"], ref)
+    print(f"\n[{arch} fp32x3 B={B}] bpp {bpp.item():.8f} ref {ref['bpp'].item():.8f} psnr {v_psnr.item():.6f} "
+          f"ref {ref['v_psnr'].item():.6f} flips {flips}")
+    assert abs(bpp.item() - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (B * 65536)
+    assert abs(v_psnr.item() - ref["v_psnr"].item()) <= 1e-4
+    check_decoder(net.last, ref, P, flips)

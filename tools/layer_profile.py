@@ -15,7 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import lic_amd.functional as Fn  # noqa: E402
 
-REC = collections.defaultdict(lambda: [0, 0.0])
+REC = collections.defaultdict(lambda: [0, 0.0, 0.0])   # calls, ms, FLOP
 
 
 def _label(name, args):
@@ -52,6 +52,12 @@ def wrap(name):
         r = REC[_label(name, args)]
         r[0] += 1
         r[1] += e0.elapsed_time(e1)
+        if name == "conv" and isinstance(out, Fn.Act) and len(args) > 1:
+            pk = args[1]
+            mi, mj = kw.get("out_hw") or (out.H, out.W)
+            if kw.get("shuffle") is True:
+                mi, mj = out.H // 2, out.W // 2
+            r[2] += 2.0 * out.B * mi * mj * pk.co * pk.ci * len(pk.dy) / max(1, pk.groups)
         return out
     setattr(Fn, name, w)
 
@@ -63,26 +69,39 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--post-processing", action="store_true")
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32", "bf16"])
+    ap.add_argument("--what", default="forward", choices=["forward", "a_model"])
     args = ap.parse_args()
     import bench
-    net = bench.build_net(args.arch, "fp16", args.size, args.batch, "cpu",
+    net = bench.build_net(args.arch, args.precision, args.size, args.batch, "cpu",
                           post_processing=args.post_processing).to("cuda")
+    if args.what == "a_model":
+        xin = Fn.Act.from_nchw(torch.rand(args.batch, 3, args.size, args.size, device="cuda") * 2 - 1, net.dtype,
+                               pad16=True)
+        run = lambda: net.a_model.run(xin)
+    else:
+        run = None
     x = torch.rand(args.batch, 3, args.size, args.size, device="cuda") * 2 - 1
     with torch.no_grad():
         print("warm-up forward", flush=True)
-        net(x, "test")
+        run() if run else net(x, "test")
         torch.cuda.synchronize()
         print("profiled forward", flush=True)
         for n in ("conv", "conv_transpose", "gdn", "win_attn", "layernorm", "rb3", "add", "copy", "avgpool",
                   "quantize_median", "gauss_rate", "syntax_recon", "bpp_finalize", "psnr_finalize",
                   "recon", "pool_partials", "ca_apply", "lam", "csam"):
             wrap(n)
-        net(x, "test")
+        run() if run else net(x, "test")
         torch.cuda.synchronize()
+    peak = {"fp16": 2516.6, "bf16": 2516.6, "fp32": 157.3}[args.precision]
     tot = sum(v[1] for v in REC.values())
-    print(f"# serialised op time {tot:.3f} ms over {sum(v[0] for v in REC.values())} ops")
-    for k, (n, t) in sorted(REC.items(), key=lambda kv: -kv[1][1])[:args.top]:
-        print(f"{t:8.3f} ms {100 * t / tot:5.1f}% x{n:<4d} {k}")
+    fl = sum(v[2] for v in REC.values())
+    print(f"# {args.what} {args.arch} {args.precision} B={args.batch} {args.size}^2: serialised op time {tot:.3f} ms "
+          f"over {sum(v[0] for v in REC.values())} ops; conv {fl / 1e9:.1f} GFLOP -> "
+          f"{fl / tot / 1e9:.1f} TFLOP/s ({100 * fl / tot / 1e9 / peak:.1f} % of {peak})")
+    for k, (n, t, f) in sorted(REC.items(), key=lambda kv: -kv[1][1])[:args.top]:
+        tf = f"{f / t / 1e9:7.1f} TF/s {100 * f / t / 1e9 / peak:5.1f}%" if f else " " * 20
+        print(f"{t:8.3f} ms {100 * t / tot:5.1f}% x{n:<4d} {tf}  {k}")
 
 
 if __name__ == "__main__":
