@@ -84,10 +84,14 @@ typedef struct lic_conv_args {
   int32_t out_shuffle;               /* 0, 2 or 3 */
   int32_t force_direct;              /* testing: force the non-MFMA kernel */
   int32_t force_mfma_generic;        /* testing: skip the spatial-tile (halo) kernel */
-  /* fp32 only: 1 = form the products on the fp16 matrix cores from fp16 parts (x_hi*W1 +
-   * x_hi*W2 + x_lo*W1, x_lo = fp16(x - fp16(x)), ~3e-7 relative per product) where a spatial-tile config applies, with
-   * wgt_split = the same weights packed [copad][ntaps][cpad/16][W1 16 | W2 16] in fp16,
-   * W1 = fp16(w)*2^11, W2 = fp16((w - fp16(w))*2^11); other launches use wgt (exact fp32). */
+  /* fp32 only, spatial-tile (k x k) launches; others use wgt (exact fp32):
+   * 0 = exact fp32-input MFMA;
+   * 2 = "fp32x6": three bf16 parts per operand (x = x0+x1+x2 exactly, split in LDS), six
+   *     products x0w0+x0w1+x1w0+x0w2+x1w1+x2w0 on the bf16 matrix cores (dropped terms <= 2^-26
+   *     relative); wgt_split = the weights as bf16 [copad][ntaps][cpad/16][w0 16 | w1 16 | w2 16];
+   * 1 = "fp32x3": fp16 parts, x_hi*W1 + x_hi*W2 + x_lo*W1 (x_lo = fp16(x - fp16(x)), ~3e-7
+   *     relative per product); wgt_split = fp16 [copad][ntaps][cpad/16][W1 16 | W2 16],
+   *     W1 = fp16(w)*2^11, W2 = fp16((w - fp16(w))*2^11). */
   int32_t mfma_mode;
   const void* wgt_split;
 } lic_conv_args;

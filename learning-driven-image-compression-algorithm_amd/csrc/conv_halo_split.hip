@@ -1,28 +1,66 @@
-// fp32 convolutions on the fp16 matrix cores ("split" MFMA mode, lic_conv_args.mfma_mode = 1).
+// fp32 convolutions on the 16-bit matrix cores ("split" MFMA modes, lic_conv_args.mfma_mode).
 //
 // The spatial-tile conv of conv_halo.h for fp32 activations, with every product formed from
-// fp16 parts on v_mfma_f32_32x32x16_f16 instead of the 16x slower fp32-input MFMA:
-//   x: x_hi = fp16(x),  x_lo = fp16(x - x_hi)                             (split in LDS)
-//   w: W1 = fp16(w) * 2^11 (exact),  W2 = fp16((w - fp16(w)) * 2^11)     (packed on the host)
-//   2^11 * x * w ~= x_hi*W1 + x_hi*W2 + x_lo*W1                          (one fp32 accumulator)
+// 16-bit parts on v_mfma_f32_32x32x16_{f16,bf16} instead of the 16x slower fp32-input MFMA.
+//
+// mfma_mode 2, "fp32x6" (bf16 parts, fp32 grade):
+//   x = x0 + x1 + x2, x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)   (split in LDS)
+//   w = w0 + w1 + w2 likewise                                                  (packed on the host)
+//   x * w ~= x0w0 + x0w1 + x1w0 + x0w2 + x1w1 + x2w0                           (one fp32 accumulator)
+// bf16 keeps fp32's exponent range and three RNE parts carry all 24 significand bits, so the
+// splits are exact (no scaling, no subnormal loss); the dropped terms x1w2 + x2w1 + x2w2 are
+// <= 2^-26 |x w|, below the fp32 rounding of the accumulation itself (2^-24).
+//
+// mfma_mode 1, "fp32x3" (fp16 parts, ~3e-7 per product):
+//   x: x_hi = fp16(x),  x_lo = fp16(x - x_hi)
+//   w: W1 = fp16(w) * 2^11 (exact),  W2 = fp16((w - fp16(w)) * 2^11)
+//   2^11 * x * w ~= x_hi*W1 + x_hi*W2 + x_lo*W1, the accumulator scaled by 2^-11 in the epilogue.
 // The dropped term (x - x_hi)(w - fp16(w)) is <= 2^-22 |x w| and each part carries 11 bits, so
 // a product is within ~3e-7 of its fp32 value (fp32 itself: 6e-8).  x_lo is an fp16 subnormal
-// for |x| < 2^-3; its absolute error stays <= 2^-25, ~2^-25 sum|w| on an output.  The fp32
-// accumulator (fp32 adds) is scaled back by 2^-11 in the epilogue.
+// for |x| < 2^-3; its absolute error stays <= 2^-25.
 //
 // Per 16-channel chunk the fp32 halo of the tile arrives by LDS-DMA in a staging buffer
 // (double-buffered, the next chunk's DMA overlaps this chunk's MFMAs); all threads then
-// split it once into an x_hi and an x_lo plane laid out as the fp16 kernel's halo (32 B per
-// pixel, halves XOR-swizzled), and every tap reads its shifted windows from the planes.
-// Weights stream as [G taps][BN][W1 32 B | W2 32 B] stages by LDS-DMA (double buffer).
+// split it once into NPA 16-bit planes laid out as the fp16 kernel's halo (32 B per pixel,
+// halves XOR-swizzled), and every tap reads its shifted windows from the planes.  Weights
+// stream as [G taps][BN][NPB planes x 32 B] stages by LDS-DMA (double buffer).
 #include "conv_halo.h"
+
+#include <cstdlib>
 
 namespace lic {
 
-constexpr float kSplitScale = 2048.0f;  // 2^11
+constexpr float kSplitScale = 2048.0f;  // 2^11 (mode 1)
 
-template <int TH, int TW, int BN, int WM, int WN>
+// SPLIT_PARTIAL: chain the products of one tap from zero and add the partial to the running sum
+// with an fp32 VALU add (else the running sum is the MFMA's C operand).  SPLIT_ALT: odd channel
+// chunks are split from -x and subtracted (see split_chunk).
+#ifndef SPLIT_PARTIAL
+#define SPLIT_PARTIAL 0
+#endif
+#ifndef SPLIT_ALT
+#define SPLIT_ALT 1
+#endif
+
+template <int MODE> struct SplitMode;
+template <> struct SplitMode<1> {   // fp16: x_hi, x_lo x W1, W2
+  using T = half_t;
+  static constexpr int NPA = 2, NPB = 2, NPROD = 3;
+  static constexpr int PA[NPROD] = {0, 0, 1}, PB[NPROD] = {0, 1, 0};
+  static constexpr float scale = 1.0f / kSplitScale;
+};
+template <> struct SplitMode<2> {   // bf16: x0, x1, x2 x w0, w1, w2
+  using T = bf16_t;
+  static constexpr int NPA = 3, NPB = 3, NPROD = 6;
+  static constexpr int PA[NPROD] = {0, 0, 1, 0, 1, 2}, PB[NPROD] = {0, 1, 0, 2, 1, 0};
+  static constexpr float scale = 1.0f;
+};
+
+template <int MODE, int TH, int TW, int BN, int WM, int WN>
 __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic_conv_args a, const HaloPlan p) {
+  using SM = SplitMode<MODE>;
+  using T = typename SM::T;
+  constexpr int NPA = SM::NPA, NPB = SM::NPB;
   constexpr int NT = WM * WN * 64;
   constexpr int BM = TH * TW;
   constexpr int CK = 16;  // fp32 channels per chunk (64 B per pixel)
@@ -32,12 +70,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int sbytes = p.hpix_pad * 64;   // fp32 staging of one chunk
-  const int pbytes = p.hpix_pad * 32;   // one fp16 plane
-  const int wbytes = p.G * BN * 64;
+  const int pbytes = p.hpix_pad * 32;   // one 16-bit plane
+  const int wbytes = p.G * BN * NPB * 32;
   char* stg0 = smem;
-  char* phi = smem + 2 * sbytes;
-  char* plo = phi + pbytes;
-  char* wbuf0 = plo + pbytes;
+  char* pl0 = smem + 2 * sbytes;        // NPA planes, pbytes apart
+  char* wbuf0 = pl0 + NPA * pbytes;
   int* rowpix = (int*)(smem + p.rp_off);
   float* sbias = (float*)(rowpix + BM);
 
@@ -67,7 +104,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
   }
 
   const float* __restrict__ xg = (const float*)a.x;
-  const half_t* __restrict__ wg = (const half_t*)a.wgt_split;
+  const T* __restrict__ wg = (const T*)a.wgt_split;
   const int nchunks = a.cpad / CK;
   const int nst = nchunks * p.ngroups;
   const int hq_total = p.hpix_pad * 4;
@@ -89,39 +126,47 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
       glds16(src, dst + q0 * 16);
     }
   };
-  // weights of stage s: slot (tt, n, s4) holds plane s4>>1 (W1 / W2), swizzled half s4&1
+  // weights of stage s: 16-B slot (tt, n, sl) holds plane sl>>1, swizzled half sl&1
   auto issue_w = [&](int s, int buf, int nw_ld) {
     const int k = s / p.ngroups, g = s - k * p.ngroups;
     const int t0 = g * p.G;
     const int gcur = min(p.G, a.ntaps - t0);
-    const int total = gcur * BN * 4;
+    const int total = gcur * BN * 2 * NPB;
     char* dst = wbuf0 + buf * wbytes;
     for (int q0 = wave * 64; q0 < total; q0 += nw_ld * 64) {
       const int q = q0 + lane;
-      const int tt = q / (BN * 4);
-      const int n = (q >> 2) - tt * BN;
-      const int slot = q & 3;
-      const int piece = (slot & 2) | ((slot & 1) ^ ((n >> 3) & 1));
-      const half_t* src = wg + ((int64_t)(n0 + n) * a.ntaps + t0 + tt) * (2 * a.cpad) + k * 32 + piece * 8;
+      const int row = q / (2 * NPB), slot = q - row * (2 * NPB);
+      const int tt = row / BN, n = row - tt * BN;
+      const int piece = (slot & ~1) | ((slot & 1) ^ ((n >> 3) & 1));
+      const T* src = wg + ((int64_t)(n0 + n) * a.ntaps + t0 + tt) * (NPB * a.cpad) + k * (16 * NPB) + piece * 8;
       glds16(src, dst + q0 * 16);
     }
   };
-  // staging -> x_hi / x_lo planes (32 B per pixel each, halves swizzled as the fp16 kernel)
-  auto split_chunk = [&](int buf) {
+  // staging -> NPA planes (32 B per pixel each, halves swizzled as the fp16 kernel).  The
+  // 16-bit MFMA's internal rounding is biased toward -inf (tools/split_accuracy.py: mean error
+  // -1.5e-8 of the output scale, exact-fp32 MFMA: 2e-10); with SPLIT_ALT the odd chunks are split
+  // from -x and their partials subtracted, so the bias of the two halves cancels.
+  auto split_chunk = [&](int buf, bool neg) {
     const char* src = stg0 + buf * sbytes;
+    const float sg = neg ? -1.f : 1.f;
+    const int pro = a.prologue;
     for (int q = tid; q < hq_total; q += NT) {
       const int hp = q >> 2, c = q & 3;
-      const float4 v = *(const float4*)(src + q * 16);
-      const float f[4] = {v.x, v.y, v.z, v.w};
-      half_t hi[4], lo[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        hi[e] = (half_t)f[e];
-        lo[e] = (half_t)(f[e] - (float)hi[e]);
-      }
+      float4 v = *(const float4*)(src + q * 16);
+      if (pro == LIC_PRO_SQUARE) v = make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
+      else if (pro == LIC_PRO_ABS) v = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
+      float r[4] = {sg * v.x, sg * v.y, sg * v.z, sg * v.w};
       const int off = hp * 32 + (((c >> 1) ^ ((hp >> 3) & 1)) << 4) + (c & 1) * 8;
-      *(uint2*)(phi + off) = *(const uint2*)hi;
-      *(uint2*)(plo + off) = *(const uint2*)lo;
+#pragma unroll
+      for (int pl = 0; pl < NPA; ++pl) {
+        T part[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          part[e] = (T)r[e];
+          r[e] -= (float)part[e];      // exact: the residual fits fp32
+        }
+        *(uint2*)(pl0 + pl * pbytes + off) = *(const uint2*)part;
+      }
     }
   };
 
@@ -151,7 +196,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
   for (int s = 0; s < nst; ++s) {
     const int k = s / p.ngroups, g = s - k * p.ngroups;
     if (g == 0) {  // a new chunk landed in staging[k & 1]: split it (all waves are past the last tap reads)
-      split_chunk(k & 1);
+#if SPLIT_ALT && !SPLIT_PARTIAL
+      if (k > 0)   // exact sign flip: the running sum changes sign with the chunk's planes
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = -acc[i][j];
+#endif
+      split_chunk(k & 1, SPLIT_ALT && (k & 1));
       __syncthreads();
     }
     constexpr int NL = HALO_LOADERS < NT / 64 ? HALO_LOADERS : NT / 64;
@@ -163,7 +215,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
     const int t0 = g * p.G;
     const int gcur = min(p.G, a.ntaps - t0);
     int cy = t0 / p.nx, cx = t0 - cy * p.nx;
-    auto load_frags = [&](int tt, u32x4(&fh)[TM], u32x4(&fl)[TM], u32x4(&f1)[TN], u32x4(&f2)[TN]) {
+    auto load_frags = [&](int tt, u32x4(&fa)[NPA][TM], u32x4(&fb)[NPB][TN]) {
       const int toff = p.toff0 + cy * p.ystep + cx * p.xstep;
       if (++cx == p.nx) {
         cx = 0;
@@ -173,41 +225,59 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
       for (int i = 0; i < TM; ++i) {
         const int hp = hbase[i] + toff;
         const int o = hp * 32 + ((lhalf ^ ((hp >> 3) & 1)) << 4);
-        fh[i] = *(const u32x4*)(phi + o);
-        fl[i] = *(const u32x4*)(plo + o);
+#pragma unroll
+        for (int pl = 0; pl < NPA; ++pl) fa[pl][i] = *(const u32x4*)(pl0 + pl * pbytes + o);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = wn * WTN + j * 32 + lrow;
-        const char* wr = wb + (tt * BN + n) * 64 + ((lhalf ^ ((n >> 3) & 1)) << 4);
-        f1[j] = *(const u32x4*)wr;
-        f2[j] = *(const u32x4*)(wr + 32);
+        const char* wr = wb + (tt * BN + n) * (NPB * 32) + ((lhalf ^ ((n >> 3) & 1)) << 4);
+#pragma unroll
+        for (int pl = 0; pl < NPB; ++pl) fb[pl][j] = *(const u32x4*)(wr + pl * 32);
       }
     };
-    auto mfmas = [&](const u32x4(&fh)[TM], const u32x4(&fl)[TM], const u32x4(&f1)[TN], const u32x4(&f2)[TN]) {
+    // Per fragment and tap the NPROD products of 16 channels are chained from zero and added to
+    // the running sum by one fp32 VALU add (round to nearest even): the 16-bit MFMA's own
+    // accumulation rounding is biased (measured: mean error -7e-9 of the output scale when the
+    // running sum is its C operand, tools/split_accuracy.py), and chaining it only over a partial
+    // of 16 x NPROD terms shrinks that bias with the partial's magnitude.
+    const bool negk = SPLIT_ALT && (k & 1);
+    auto mfmas = [&](const u32x4(&fa)[NPA][TM], const u32x4(&fb)[NPB][TN]) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = mfma_k16<half_t>(fh[i], f1[j], acc[i][j]);
-          acc[i][j] = mfma_k16<half_t>(fh[i], f2[j], acc[i][j]);
-          acc[i][j] = mfma_k16<half_t>(fl[i], f1[j], acc[i][j]);
+#if SPLIT_PARTIAL
+          floatx16 t = mfma_k16<T>(fa[SM::PA[SM::NPROD - 1]][i], fb[SM::PB[SM::NPROD - 1]][j], floatx16{});
+#pragma unroll
+          for (int pr = SM::NPROD - 2; pr >= 0; --pr)   // smallest terms first
+            t = mfma_k16<T>(fa[SM::PA[pr]][i], fb[SM::PB[pr]][j], t);
+          if (negk) acc[i][j] -= t;
+          else acc[i][j] += t;
+#else
+          // running sum as C; it holds -sum through the odd chunks (flipped at chunk starts)
+#pragma unroll
+          for (int pr = SM::NPROD - 1; pr >= 0; --pr)
+            acc[i][j] = mfma_k16<T>(fa[SM::PA[pr]][i], fb[SM::PB[pr]][j], acc[i][j]);
+#endif
         }
     };
-    u32x4 fh[2][TM], fl[2][TM], f1[2][TN], f2[2][TN];
-    load_frags(0, fh[0], fl[0], f1[0], f2[0]);
+    u32x4 fa[2][NPA][TM], fb[2][NPB][TN];
+    load_frags(0, fa[0], fb[0]);
     int tt = 0;
     for (; tt + 2 <= gcur; tt += 2) {
-      load_frags(tt + 1, fh[1], fl[1], f1[1], f2[1]);
-      mfmas(fh[0], fl[0], f1[0], f2[0]);
-      load_frags(tt + 2, fh[0], fl[0], f1[0], f2[0]);   // past the group's last tap: discarded
-      mfmas(fh[1], fl[1], f1[1], f2[1]);
+      load_frags(tt + 1, fa[1], fb[1]);
+      mfmas(fa[0], fb[0]);
+      load_frags(tt + 2, fa[0], fb[0]);   // past the group's last tap: discarded
+      mfmas(fa[1], fb[1]);
     }
-    if (tt < gcur) mfmas(fh[0], fl[0], f1[0], f2[0]);
+    if (tt < gcur) mfmas(fa[0], fb[0]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
+  // with SPLIT_ALT and the running sum as C, an even chunk count leaves it negated
+  const float oscale = (!SPLIT_PARTIAL && SPLIT_ALT && nchunks > 0 && !(nchunks & 1)) ? -SM::scale : SM::scale;
   float* ct = (float*)smem + wave * (32 * 33);
   epilogue_all<float, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, [&](int q) {
 #pragma unroll
@@ -215,12 +285,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
       if (qq == q) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * (1.0f / kSplitScale);
+          ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * oscale;
       }
   });
 }
 
-template <int TH, int TW, int BN, int WM, int WN>
+template <int MODE, int TH, int TW, int BN, int WM, int WN>
 static int try_halo_split(const lic_conv_args& a, hipStream_t s, int& status) {
   constexpr int NT = WM * WN * 64;
   if (a.copad % BN || a.cpad % 16 || a.ci % 4 || a.ldx % 4 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt_split % 16))
@@ -240,9 +310,10 @@ static int try_halo_split(const lic_conv_args& a, hipStream_t s, int& status) {
   const int hpix = p.hh * p.hw;
   if (hpix > 32767) return 0;
   p.hpix_pad = (hpix + 31) / 32 * 32;
-  const int fixed = 2 * p.hpix_pad * 64 + 2 * p.hpix_pad * 32;
+  constexpr int NPA = SplitMode<MODE>::NPA, NPB = SplitMode<MODE>::NPB;
+  const int fixed = 2 * p.hpix_pad * 64 + NPA * p.hpix_pad * 32;
   const int budget = 160 * 1024 - fixed - TH * TW * 4 - BN * 4;
-  int G = budget / (2 * BN * 64);
+  int G = budget / (2 * BN * NPB * 32);
   if (G < 1) return 0;
   if (G > a.ntaps) G = a.ntaps;
   p.G = G;
@@ -261,14 +332,14 @@ static int try_halo_split(const lic_conv_args& a, hipStream_t s, int& status) {
   p.ystep = sy * p.hw;
   p.xstep = sx;
   const int epi_bytes = (NT / 64) * 32 * 33 * 4;
-  p.rp_off = fixed + 2 * G * BN * 64;
+  p.rp_off = fixed + 2 * G * BN * NPB * 32;
   if (p.rp_off < epi_bytes) p.rp_off = epi_bytes;
   const int smem = p.rp_off + TH * TW * 4 + BN * 4;
   p.smem = smem;
   if (smem > 160 * 1024) return 0;
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   dim3 grid((unsigned)blocks, a.copad / BN);
-  auto kern = conv_halo_split_kernel<TH, TW, BN, WM, WN>;
+  auto kern = conv_halo_split_kernel<MODE, TH, TW, BN, WM, WN>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
     status = fail(std::string("halo split conv: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -280,21 +351,33 @@ static int try_halo_split(const lic_conv_args& a, hipStream_t s, int& status) {
   return 1;
 }
 
-// Returns 1 and launches when a split tile config applies (fp32, mfma_mode 1, k x k taps),
-// 0 to let the caller run the exact-fp32 kernels.
-int conv_halo_split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
-  if (a.mfma_mode != 1 || !a.wgt_split || a.dtype != LIC_F32) return 0;
-  if (a.groups != 1 || a.ntaps < 2 || a.prologue != LIC_PRO_NONE || a.force_direct || a.force_mfma_generic) return 0;
+template <int MODE>
+static int split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   auto blocks = [&](int th, int tw, int bn) {
     return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
   };
+  // each try returns 0 without launching when its LDS plan does not fit (e.g. stride-2 halos)
   if (a.mi > 8 && a.mj > 8) {
-    if (a.copad % 192 == 0 && blocks(16, 16, 192) >= 200) return try_halo_split<16, 16, 192, 4, 2>(a, s, status);
-    if (a.copad % 128 == 0 && blocks(16, 16, 128) >= 200) return try_halo_split<16, 16, 128, 4, 2>(a, s, status);
-    if (a.copad % 64 == 0 && blocks(16, 16, 64) >= 200) return try_halo_split<16, 16, 64, 4, 2>(a, s, status);
+    static const bool no192 = getenv("LIC_SPLIT_NO192") != nullptr;   // tuning probe
+    if (MODE == 1 && !no192 && a.copad % 192 == 0 && blocks(16, 16, 192) >= 200 &&
+        try_halo_split<MODE, 16, 16, 192, 4, 2>(a, s, status))
+      return 1;
+    if (a.copad % 128 == 0 && blocks(16, 16, 128) >= 200 && try_halo_split<MODE, 16, 16, 128, 4, 2>(a, s, status))
+      return 1;
+    if (a.copad % 64 == 0 && blocks(16, 16, 64) >= 200 && try_halo_split<MODE, 16, 16, 64, 4, 2>(a, s, status))
+      return 1;
   }
-  if (a.copad % 64 == 0 && blocks(8, 8, 64) >= 128) return try_halo_split<8, 8, 64, 2, 2>(a, s, status);
+  if (a.copad % 64 == 0 && blocks(8, 8, 64) >= 128 && try_halo_split<MODE, 8, 8, 64, 2, 2>(a, s, status)) return 1;
   return 0;
+}
+
+// Returns 1 and launches when a split tile config applies (fp32, mfma_mode 1 / 2, k x k taps incl. 1x1),
+// 0 to let the caller run the exact-fp32 kernels.
+int conv_halo_split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
+  if ((a.mfma_mode != 1 && a.mfma_mode != 2) || !a.wgt_split || a.dtype != LIC_F32) return 0;
+  if (a.groups != 1 || a.ntaps < 1 || a.force_direct || a.force_mfma_generic) return 0;
+  if (a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE && a.prologue != LIC_PRO_ABS) return 0;
+  return a.mfma_mode == 1 ? split_dispatch<1>(a, s, status) : split_dispatch<2>(a, s, status);
 }
 
 }  // namespace lic

@@ -263,21 +263,23 @@ def _ptr(a: Optional[Act]):
     return (a.ptr, a.ld) if a is not None else (None, 0)
 
 
-# fp32 convolutions on the fp16 matrix cores (lic_conv_args.mfma_mode = 1, conv_halo_split.hip):
-# on while a Net with precision='fp32x3' runs (split_f32 context), off otherwise.
-_SPLIT_F32 = [False]
+# fp32 convolutions on the 16-bit matrix cores (lic_conv_args.mfma_mode, conv_halo_split.hip):
+# mode 2 ("fp32x6": three bf16 parts per operand, six products, fp32 grade) while a Net with
+# precision='fp32x6' runs, mode 1 ("fp32x3": fp16 parts, three products) for 'fp32x3', 0 otherwise.
+_SPLIT_F32 = [0]
+SPLIT_MODES = {"fp32x3": 1, "fp32x6": 2}
 
 
 class split_f32:
-    """Context: fp32 spatial-tile convolutions form their products from fp16 parts on the fp16
-    MFMA (x_hi*W1 + x_hi*W2 + x_lo*W1, include/lic.h mfma_mode)."""
+    """Context: fp32 spatial-tile convolutions form their products from 16-bit parts on the
+    fp16 / bf16 MFMA (include/lic.h mfma_mode).  `mode`: 0 off, 1 fp32x3, 2 fp32x6 (True = 1)."""
 
-    def __init__(self, enabled: bool = True):
-        self.enabled = enabled
+    def __init__(self, mode=1):
+        self.mode = int(mode)
 
     def __enter__(self):
         self.prev = _SPLIT_F32[0]
-        _SPLIT_F32[0] = self.enabled
+        _SPLIT_F32[0] = self.mode
         return self
 
     def __exit__(self, *exc):
@@ -285,26 +287,36 @@ class split_f32:
         return False
 
 
-def split_weights(pk: ConvPack) -> Optional[torch.Tensor]:
-    """The fp16 split pack of an fp32 ConvPack ([copad][ntaps][cpad/16][W1 16 | W2 16],
-    W1 = fp16(w) * 2^11, W2 = fp16((w - fp16(w)) * 2^11)), cached on the pack; None when a
-    weight is too large for W1 (|w| >= 31)."""
-    sw = pk.__dict__.get("_split")
+def split_weights(pk: ConvPack, mode: int = 1) -> Optional[torch.Tensor]:
+    """The 16-bit split pack of an fp32 ConvPack, cached on the pack:
+    mode 1: fp16 [copad][ntaps][cpad/16][W1 16 | W2 16], W1 = fp16(w) * 2^11,
+            W2 = fp16((w - fp16(w)) * 2^11); None when a weight is too large for W1 (|w| >= 31);
+    mode 2: bf16 [copad][ntaps][cpad/16][w0 16 | w1 16 | w2 16], w = w0 + w1 + w2 exactly
+            (w0 = bf16(w), w1 = bf16(w - w0), w2 = bf16(w - w0 - w1), round to nearest even)."""
+    key = "_split%d" % mode
+    sw = pk.__dict__.get(key)
     if sw is not None and sw[0] is pk.w and sw[1] == pk.w._version:
         return sw[2]
     w = pk.w
     if w.dtype != torch.float32 or w.shape[2] % 16:
         return None
-    if float(w.abs().max()) >= 31.0:
+    co, nt, cp = w.shape
+    if mode == 2:
+        parts, r = [], w
+        for _ in range(3):
+            q = r.to(torch.bfloat16)
+            parts.append(q.view(co, nt, cp // 16, 16))
+            r = r - q.float()
+        out = torch.cat(parts, -1).reshape(co, nt, 3 * cp).contiguous()
+    elif float(w.abs().max()) >= 31.0:
         out = None
     else:
         hi = w.half()
         w1 = (hi.float() * 2048.0).half()
         w2 = ((w - hi.float()) * 2048.0).half()
-        co, nt, cp = w.shape
         out = torch.cat([w1.view(co, nt, cp // 16, 16), w2.view(co, nt, cp // 16, 16)], -1).reshape(co, nt, 2 * cp)
         out = out.contiguous()
-    pk.__dict__["_split"] = (pk.w, pk.w._version, out)
+    pk.__dict__[key] = (pk.w, pk.w._version, out)
     return out
 
 
@@ -356,10 +368,10 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     a.out_shuffle = mode
     a.force_direct = 1 if force_direct else 0
     a.force_mfma_generic = 1 if force_generic else 0
-    if _SPLIT_F32[0] and x.dtype == torch.float32 and pk.groups == 1 and nt >= 2 and prologue == _ffi.PRO_NONE:
-        ws = split_weights(pk)
+    if _SPLIT_F32[0] and x.dtype == torch.float32 and pk.groups == 1:
+        ws = split_weights(pk, _SPLIT_F32[0])
         if ws is not None:
-            a.mfma_mode, a.wgt_split = 1, _dp(ws)
+            a.mfma_mode, a.wgt_split = _SPLIT_F32[0], _dp(ws)
     check(_lib().lic_conv2d_fwd(ctypes.byref(a), stream_handle()))
     return out
 

@@ -358,10 +358,10 @@ _IGNORED_PREFIXES = ("y_sampler.", "h_sampler.", "test_y_sampler.", "test_h_samp
 
 class Net(nn.Module):
     """net_ga.Net (net_ga.py:735-1144).  ``precision`` selects the activation dtype of
-    the HIP path: 'fp32' (parity, exact-fp32 MFMA), 'fp32x3' (fp32 activations whose spatial-tile
-    convolutions form each product from fp16 parts on the fp16 matrix cores, ~3e-7 relative;
-    csrc/conv_halo_split.hip), 'fp16' or 'bf16' (fp32 accumulation; bf16 is the training
-    precision of BASELINE config 5)."""
+    the HIP path: 'fp32' (parity, exact-fp32 MFMA), 'fp32x6' / 'fp32x3' (fp32 activations whose
+    spatial-tile convolutions form each product from three bf16 parts per operand -- fp32 grade --
+    or two fp16 parts, ~3e-7 relative, on the 16-bit matrix cores; csrc/conv_halo_split.hip),
+    'fp16' or 'bf16' (fp32 accumulation; bf16 is the training precision of BASELINE config 5)."""
 
     arch = "net_ga"
 
@@ -375,8 +375,8 @@ class Net(nn.Module):
         self.test_size = test_size
         self.post_processing = post_processing
         self.is_high = is_high
-        if precision not in ("fp32", "fp32x3", "fp16", "bf16"):
-            raise ValueError(f"precision must be 'fp32', 'fp32x3', 'fp16' or 'bf16', got {precision!r}")
+        if precision not in ("fp32", "fp32x6", "fp32x3", "fp16", "bf16"):
+            raise ValueError(f"precision must be 'fp32', 'fp32x6', 'fp32x3', 'fp16' or 'bf16', got {precision!r}")
         self.precision = precision
         N, M = (384, 32) if is_high else (192, 16)
         self.M, self.N = M, N
@@ -602,7 +602,7 @@ class Net(nn.Module):
         return self.__dict__["_coder"][1]
 
     def compress(self, inputs: torch.Tensor):
-        with torch.no_grad(), Fn.split_f32(self.precision == "fp32x3"):
+        with torch.no_grad(), Fn.split_f32(Fn.SPLIT_MODES.get(self.precision, 0)):
             return self._compress(inputs)
 
     def _compress(self, inputs: torch.Tensor):
@@ -636,7 +636,7 @@ class Net(nn.Module):
                 "shape": (z.H, z.W), "syntax": syntax.cpu(), "symbols": SYM}
 
     def decompress(self, strings, shape, syntax: torch.Tensor, device="cuda"):
-        with torch.no_grad(), Fn.split_f32(self.precision == "fp32x3"):
+        with torch.no_grad(), Fn.split_f32(Fn.SPLIT_MODES.get(self.precision, 0)):
             return self._decompress(strings, shape, syntax, device)
 
     def _decompress(self, strings, shape, syntax: torch.Tensor, device="cuda"):
@@ -762,7 +762,7 @@ class Net(nn.Module):
             return net_forward_train(self, inputs, seed, seed_dev)
         if mode != 'test':
             raise ValueError(f"mode must be 'train' or 'test', got {mode!r}")
-        with torch.no_grad(), Fn.split_f32(self.precision == "fp32x3"):
+        with torch.no_grad(), Fn.split_f32(Fn.SPLIT_MODES.get(self.precision, 0)):
             return self._forward_test(inputs, return_intermediates, noise_seed)
 
     def _forward_test(self, inputs: torch.Tensor, return_intermediates: bool, noise_seed: Optional[int] = None):

@@ -1,6 +1,8 @@
-"""precision='fp32x3': fp32 activations whose spatial-tile convolutions form every product
-from fp16 parts on the fp16 matrix cores (csrc/conv_halo_split.hip; include/lic.h mfma_mode):
-2^11 x w ~= x_hi*W1 + x_hi*W2 + x_lo*W1 (x_hi = fp16(x), x_lo = fp16(x - x_hi)), ~3e-7 relative per product (fp32: 6e-8).
+"""precision='fp32x6' / 'fp32x3': fp32 activations whose spatial-tile convolutions form every
+product from 16-bit parts on the matrix cores (csrc/conv_halo_split.hip; include/lic.h mfma_mode):
+fp32x6 = three exact bf16 parts per operand, six products (dropped terms <= 2^-26 relative);
+fp32x3 = 2^11 x w ~= x_hi*W1 + x_hi*W2 + x_lo*W1 (x_hi = fp16(x), x_lo = fp16(x - x_hi)), ~3e-7
+relative per product (fp32: 6e-8).
 
 Bars: per kernel, max error <= 3e-6 of the output scale against torch fp32 on the CPU and
 <= 5e-6 against the exact-fp32 MFMA kernel on the same pack (both sides carry rounding error); end to end, the fp32 parity bars
@@ -16,6 +18,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.mark.parametrize("mode", [2, 1])
 @pytest.mark.parametrize("cin,cout,k,s,pad,B,H,epi", [
     (192, 192, 3, 1, (1, 1, 1, 1), 8, 64, "plain"),    # WNSA conv3x3 (16x16 x 192 tiles)
     (192, 192, 7, 1, (3, 3, 3, 3), 8, 64, "lrelu_r1"),  # conv7x7, tap groups
@@ -23,8 +26,11 @@ DEV = "cuda"
     (192, 192, 3, 1, (1, 1, 1, 1), 32, 16, "gelu"),    # slice-loop latents (8x8 x 64 tiles)
     (128, 64, 3, 1, (1, 1, 1, 1), 32, 16, "gate"),     # 8x8 tiles, 64-wide blocks, gate epilogue
     (96, 128, 3, 1, (1, 1, 1, 1), 8, 50, "plain"),     # ragged map, 16x16 x 64 tiles
+    (192, 576, 1, 1, (0, 0, 0, 0), 32, 64, "plain"),   # 1x1 qkv Linear of Win_noShift_Attention
+    (192, 192, 1, 2, (0, 0, 0, 0), 8, 128, "plain"),   # 1x1 s2 skip of ResidualBlockWithStride (8x8 tiles)
+    (192, 192, 1, 1, (0, 0, 0, 0), 8, 128, "square"),  # GDN: conv1x1(x^2) (prologue SQUARE)
 ])
-def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi):
+def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     import lic_amd.functional as Fn
     from lic_amd import _ffi as L
     from lic_amd.layers import Conv2d
@@ -39,41 +45,67 @@ def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi):
     r = Fn.Act.from_nchw(torch.randn(B, cout, Ho, Wo).to(DEV), torch.float32)
     g = Fn.Act.from_nchw(torch.rand(B, cout, Ho, Wo).to(DEV), torch.float32)
     kw = {"plain": {}, "gelu": dict(act=L.ACT_GELU), "lrelu_r1": dict(act=L.ACT_LRELU, r1=r),
+          "square": dict(prologue=L.PRO_SQUARE),
           "gate": dict(act=L.ACT_LRELU, epi=L.EPI_GATE, g=g, r2=r, r1=r)}[epi]
     exact = Fn.conv(X, pk, **kw).nchw().cpu()
-    with Fn.split_f32(True):
+    with Fn.split_f32(mode):
         got = Fn.conv(X, pk, **kw).nchw().cpu()
-    assert Fn.split_weights(pk) is not None
+    ws = Fn.split_weights(pk, mode)
+    assert ws is not None
+    if mode == 2:    # the three bf16 parts sum to the fp32 weights exactly
+        co, nt, cp = pk.w.shape
+        parts = ws.view(co, nt, cp // 16, 3, 16).float().sum(3).reshape(co, nt, cp)
+        assert torch.equal(parts, pk.w)
     scale = exact.abs().max().item()
     err = (got - exact).abs().max().item()
     base = F.conv2d(F.pad(x, (pad[1], pad[3], pad[0], pad[2])), m.weight.detach().cpu(), m.bias.detach().cpu(), s)
-    err_cpu = (got - {"plain": base, "gelu": F.gelu(base), "lrelu_r1": None, "gate": None}[epi]).abs().max().item() \
-        if epi in ("plain", "gelu") else 0.0
-    print(f"\n[split conv{k}x{k} {cin}->{cout} B={B} {H}^2 {epi}] max err vs exact-fp32 kernel {err:.2e}, "
+    if epi == "square":
+        base = F.conv2d(x * x, m.weight.detach().cpu(), m.bias.detach().cpu(), s)
+    err_cpu = (got - {"plain": base, "gelu": F.gelu(base), "square": base}[epi]).abs().max().item() \
+        if epi in ("plain", "gelu", "square") else 0.0
+    print(f"\n[split{mode} conv{k}x{k} {cin}->{cout} B={B} {H}^2 {epi}] max err vs exact-fp32 kernel {err:.2e}, "
           f"vs torch {err_cpu:.2e} (scale {scale:.2f})")
     assert not torch.equal(got, exact)          # the split kernel ran
     assert err <= 5e-6 * scale and err_cpu <= 3e-6 * scale
 
 
-def _net(arch, B=1, S=256, seed=0):
+def _net(arch, B=1, S=256, seed=0, precision="fp32x3"):
     from lic_amd.model import net_ga, net_unet_ha_hs
     torch.manual_seed(seed)
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
-    return net_ga.synthetic_syntax_bias_(mod.Net((B, S, S, 3), (B, S, S, 3), False, False, precision="fp32x3"), seed)
+    return net_ga.synthetic_syntax_bias_(mod.Net((B, S, S, 3), (B, S, S, 3), False, False, precision=precision), seed)
 
 
+@pytest.mark.parametrize("precision", ["fp32x6", "fp32x3"])
 @pytest.mark.parametrize("arch,B", [("net_ga", 1), ("net_unet_ha_hs", 1), ("net_ga", 32)])
-def test_fp32x3_net_parity(arch, B):
-    net = _net(arch, B)
-    P = {k: v.detach().float() for k, v in net.state_dict().items()}
-    net = net.to(DEV)
+def test_split_net_parity(arch, B, precision):
+    """End to end against the oracle, next to the exact-fp32 path on the same weights and input:
+    bpp 1e-5 / PSNR 1e-4 dB / decoder pinned, every symbol flip a near-tie (tests/parity.py), no
+    more flips than the exact-fp32 path + 2 (this input: both flip the same near-ties at B=1,
+    tools/split_net_accuracy.py), and an RMS error of the latent y no larger than 1.25x the
+    exact path's."""
+    net0 = _net(arch, B, precision="fp32")
+    P = {k: v.detach().float() for k, v in net0.state_dict().items()}
     x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(123 + B)) * 2 - 1
-    bpp, v_mse, v_psnr = net(x.to(DEV), "test", return_intermediates=True)
-    torch.cuda.synchronize()
     ref = R.net_forward(x, P, arch=arch)
-    flips = check_symbols(net.last["symbols"], ref)
-    print(f"\n[{arch} fp32x3 B={B}] bpp {bpp.item():.8f} ref {ref['bpp'].item():.8f} psnr {v_psnr.item():.6f} "
-          f"ref {ref['v_psnr'].item():.6f} flips {flips}")
-    assert abs(bpp.item() - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (B * 65536)
-    assert abs(v_psnr.item() - ref["v_psnr"].item()) <= 1e-4
-    check_decoder(net.last, ref, P, flips)
+    res = {}
+    for prec in ("fp32", precision):
+        net = _net(arch, B, precision=prec)
+        net.load_state_dict(net0.state_dict())
+        net = net.to(DEV)
+        bpp, v_mse, v_psnr = net(x.to(DEV), "test", return_intermediates=True)
+        torch.cuda.synchronize()
+        ne = int((net.last["symbols"].cpu() != ref["symbols"]).sum())
+        ez = (net.last["z3"].float().cpu() - ref["z3"]).pow(2).mean().sqrt().item()
+        res[prec] = (bpp.item(), v_psnr.item(), ne, ez, dict(net.last))
+        del net
+    bpp, psnr, flips, ez, last = res[precision]
+    flips0, ez0 = res["fp32"][2], res["fp32"][3]
+    print(f"\n[{arch} {precision} B={B}] bpp {bpp:.8f} ref {ref['bpp'].item():.8f} psnr {psnr:.6f} "
+          f"ref {ref['v_psnr'].item():.6f} flips {flips} (exact fp32: {flips0}) y rms err {ez:.2e} (exact fp32: {ez0:.2e})")
+    check_symbols(last["symbols"], ref, max_rate=max(3e-5, (flips0 + 2.5) / ref["symbols"].numel()))
+    assert flips <= flips0 + 2
+    assert ez <= 1.25 * ez0
+    assert abs(bpp - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (B * 65536)
+    assert abs(psnr - ref["v_psnr"].item()) <= 1e-4
+    check_decoder(last, ref, P, flips)

@@ -11,7 +11,7 @@ for o in $C/build/*.o; do
   hit=0
   for f in "$@"; do [ "$(basename $f .hip)" = "$b" ] && hit=1; done
   if [ $hit = 1 ]; then
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-function -Wno-unused-variable $defs -c $C/$b.hip -o $out/$b.o
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-function -Wno-unused-variable -Xclang -target-feature -Xclang -packed-fp32-ops $defs -c $C/$b.hip -o $out/$b.o
     objs="$objs $out/$b.o"
   else objs="$objs $o"; fi
 done

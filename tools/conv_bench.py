@@ -14,7 +14,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PEAK = {"fp16": 2516.6, "fp32": 157.3, "fp32x3": 2516.6 / 3}
+PEAK = {"fp16": 2516.6, "fp32": 157.3, "fp32x3": 2516.6 / 3, "fp32x6": 2516.6 / 6}
 
 # (name, cin, cout, k, stride, pad(t,l,b,r), H_in)   at 256x256 input
 SHAPES = [
@@ -39,7 +39,7 @@ def main():
     import lic_amd.functional as Fn
     from lic_amd.layers import Conv2d
     dt = torch.float16 if args.dtype == "fp16" else torch.float32
-    Fn._SPLIT_F32[0] = args.dtype == "fp32x3"   # fp32 activations, fp16x3 split products
+    Fn._SPLIT_F32[0] = Fn.SPLIT_MODES.get(args.dtype, 0)   # fp32 activations, 16-bit split products
     dev = "cuda"
     st = torch.cuda.current_stream()
     for name, ci, co, k, s, pad, H in SHAPES:

@@ -69,7 +69,7 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--post-processing", action="store_true")
-    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32", "bf16"])
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32", "bf16", "fp32x3", "fp32x6"])
     ap.add_argument("--what", default="forward", choices=["forward", "a_model"])
     args = ap.parse_args()
     import bench
@@ -78,7 +78,9 @@ def main():
     if args.what == "a_model":
         xin = Fn.Act.from_nchw(torch.rand(args.batch, 3, args.size, args.size, device="cuda") * 2 - 1, net.dtype,
                                pad16=True)
-        run = lambda: net.a_model.run(xin)
+        def run():
+            with Fn.split_f32(Fn.SPLIT_MODES.get(args.precision, 0)):
+                return net.a_model.run(xin)
     else:
         run = None
     x = torch.rand(args.batch, 3, args.size, args.size, device="cuda") * 2 - 1
@@ -93,7 +95,7 @@ def main():
             wrap(n)
         run() if run else net(x, "test")
         torch.cuda.synchronize()
-    peak = {"fp16": 2516.6, "bf16": 2516.6, "fp32": 157.3}[args.precision]
+    peak = {"fp16": 2516.6, "bf16": 2516.6, "fp32": 157.3, "fp32x3": 2516.6 / 3, "fp32x6": 2516.6 / 6}[args.precision]
     tot = sum(v[1] for v in REC.values())
     fl = sum(v[2] for v in REC.values())
     print(f"# {args.what} {args.arch} {args.precision} B={args.batch} {args.size}^2: serialised op time {tot:.3f} ms "
