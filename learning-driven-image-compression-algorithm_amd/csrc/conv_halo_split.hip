@@ -26,8 +26,6 @@
 // stream as [G taps][BN][NPB planes x 32 B] stages by LDS-DMA (double buffer).
 #include "conv_halo.h"
 
-#include <cstdlib>
-
 namespace lic {
 
 constexpr float kSplitScale = 2048.0f;  // 2^11 (mode 1)
@@ -358,8 +356,9 @@ static int split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   };
   // each try returns 0 without launching when its LDS plan does not fit (e.g. stride-2 halos)
   if (a.mi > 8 && a.mj > 8) {
-    static const bool no192 = getenv("LIC_SPLIT_NO192") != nullptr;   // tuning probe
-    if (MODE == 1 && !no192 && a.copad % 192 == 0 && blocks(16, 16, 192) >= 200 &&
+    // 16x16 x 192 (8 waves of 64 px x 96 ch) fits the fp32x3 fragments in 256 VGPRs; a 4-wave
+    // 128 px x 96 ch variant (acc in AGPRs, 1 wave per SIMD) measured 23 % slower
+    if (MODE == 1 && a.copad % 192 == 0 && blocks(16, 16, 192) >= 200 &&
         try_halo_split<MODE, 16, 16, 192, 4, 2>(a, s, status))
       return 1;
     if (a.copad % 128 == 0 && blocks(16, 16, 128) >= 200 && try_halo_split<MODE, 16, 16, 128, 4, 2>(a, s, status))
