@@ -500,7 +500,6 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(const lic_attn_args a
     sv[t * dp + c] = to_f(q[2 * a.c]);
     sdo[t * dp + c] = to_f(dout[p * lddo + h * d + c]);
   }
-  for (int r = tid; r < R; r += 256) stab[r] = 0.f;
   __syncthreads();
 
   const float scale = a.scale;
@@ -571,9 +570,18 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(const lic_attn_args a
     for (int c = 0; c < d; ++c) dpv += sdo[i * dp + c] * sv[j * dp + c];
     const float ds = sP[i * (N + 1) + j] * (dpv - sD[i]);
     sP[i * (N + 1) + j] = ds;
-    atomicAdd(&stab[relidx(i, j)], ds);
   }
   __syncthreads();
+  // table gradient: every relative offset r sums its (i, j) pairs in a fixed order (deterministic;
+  // an LDS atomicAdd here made training runs differ in the last bits)
+  for (int r = tid; r < R; r += 256) {
+    const int dy = r / (2 * ws - 1) - (ws - 1), dx = r % (2 * ws - 1) - (ws - 1);
+    float acc = 0.f;
+    for (int iy = max(0, dy); iy < min(ws, ws + dy); ++iy)
+      for (int ix = max(0, dx); ix < min(ws, ws + dx); ++ix)
+        acc += sP[(iy * ws + ix) * (N + 1) + (iy - dy) * ws + (ix - dx)];
+    stab[r] = acc;
+  }
   for (int e = tid; e < N * d; e += 256) {
     const int i = e / d, c = e % d;
     float aq = 0.f, ak = 0.f;
