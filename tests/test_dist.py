@@ -80,7 +80,8 @@ def _ddp_worker(rank, world, port, q):
         x = torch.randn(6, 8, generator=torch.Generator().manual_seed(100 * step + rank))
         model(x).pow(2).sum().backward()
         sync.finish()
-    q.put((rank, [None if p.grad is None else p.grad.clone() for p in params]))
+    # numpy, not tensors: torch's fd-sharing pickler needs the child alive until the parent reads
+    q.put((rank, [None if p.grad is None else p.grad.numpy().copy() for p in params]))
     D.finish(world)
 
 
@@ -110,7 +111,7 @@ def test_world2_grad_allreduce_gloo():
     for r in range(world):
         got = out[r]
         for g_, m_ in zip(got[:4], mean):
-            torch.testing.assert_close(g_, m_, rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(g_), m_, rtol=1e-5, atol=1e-6)
         assert got[4] is None and got[5] is None
 
 

@@ -25,6 +25,15 @@ SHAPES = [
     ("qkv1x1@64", 192, 576, 1, 1, (0, 0, 0, 0), 64),
     ("rbneck3x3_96@64", 96, 96, 3, 1, (1, 1, 1, 1), 64),
     ("han3x3_64@256", 64, 64, 3, 1, (1, 1, 1, 1), 256),
+    # slice loop / hyper shapes on the 16x16 latent
+    ("ru3x3_64@16", 64, 64, 3, 1, (1, 1, 1, 1), 16),
+    ("wnsa3x3@16", 192, 192, 3, 1, (1, 1, 1, 1), 16),
+    ("cc3x3_224_128@16", 224, 128, 3, 1, (1, 1, 1, 1), 16),
+    ("cc3x3_128_48@16", 128, 48, 3, 1, (1, 1, 1, 1), 16),
+    ("cc3x3_336_224@16", 336, 224, 3, 1, (1, 1, 1, 1), 16),
+    ("ru1x1_128_64@16", 128, 64, 1, 1, (0, 0, 0, 0), 16),
+    ("ru1x1_64_128@16", 64, 128, 1, 1, (0, 0, 0, 0), 16),
+    ("lin512_128@16", 512, 128, 1, 1, (0, 0, 0, 0), 16),
 ]
 
 
