@@ -366,6 +366,11 @@ static int split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     if (a.copad % 64 == 0 && blocks(16, 16, 64) >= 200 && try_halo_split<MODE, 16, 16, 64, 4, 2>(a, s, status))
       return 1;
   }
+  // stride-2 5x5 (ZeroPad + conv5x5 s2 at 128^2 -> 64^2) and other halos too large for a 16x16 tile:
+  // 8x8 x 192 stages each halo once for all 192 output channels instead of three times
+  if (MODE == 1 && a.copad % 192 == 0 && blocks(8, 8, 192) >= 512 &&
+      try_halo_split<MODE, 8, 8, 192, 2, 2>(a, s, status))
+    return 1;
   if (a.copad % 64 == 0 && blocks(8, 8, 64) >= 128 && try_halo_split<MODE, 8, 8, 64, 2, 2>(a, s, status)) return 1;
   return 0;
 }

@@ -22,7 +22,7 @@ DEV = "cuda"
 @pytest.mark.parametrize("cin,cout,k,s,pad,B,H,epi", [
     (192, 192, 3, 1, (1, 1, 1, 1), 8, 64, "plain"),    # WNSA conv3x3 (16x16 x 192 tiles)
     (192, 192, 7, 1, (3, 3, 3, 3), 8, 64, "lrelu_r1"),  # conv7x7, tap groups
-    (192, 192, 5, 2, (1, 1, 2, 2), 4, 128, "plain"),   # ZeroPad2d((1,2,1,2)) + conv5x5 s2
+    (192, 192, 5, 2, (1, 1, 2, 2), 8, 128, "plain"),   # ZeroPad2d((1,2,1,2)) + conv5x5 s2 (8x8 x 192 tiles)
     (192, 192, 3, 1, (1, 1, 1, 1), 32, 16, "gelu"),    # slice-loop latents (8x8 x 64 tiles)
     (128, 64, 3, 1, (1, 1, 1, 1), 32, 16, "gate"),     # 8x8 tiles, 64-wide blocks, gate epilogue
     (96, 128, 3, 1, (1, 1, 1, 1), 8, 50, "plain"),     # ragged map, 16x16 x 64 tiles
