@@ -39,6 +39,9 @@ constexpr float kSplitScale = 2048.0f;  // 2^11 (mode 1)
 #ifndef SPLIT_ALT
 #define SPLIT_ALT 1
 #endif
+#ifndef SPLIT_SMALL_2WG
+#define SPLIT_SMALL_2WG 1
+#endif
 
 template <int MODE> struct SplitMode;
 template <> struct SplitMode<1> {   // fp16: x_hi, x_lo x W1, W2
@@ -313,6 +316,12 @@ static int try_halo_split(const lic_conv_args& a, hipStream_t s, int& status) {
   const int budget = 160 * 1024 - fixed - TH * TW * 4 - BN * 4;
   int G = budget / (2 * BN * NPB * 32);
   if (G < 1) return 0;
+  // 8x8 x 64 (the 16x16 latents: a few hundred workgroups): fewer taps per weight stage so that two
+  // workgroups fit a CU's LDS and the whole grid is resident at once
+  if (SPLIT_SMALL_2WG && TH * TW == 64 && BN == 64) {
+    const int g2 = (80 * 1024 - fixed - TH * TW * 4 - BN * 4) / (2 * BN * NPB * 32);
+    if (g2 >= 1 && g2 < G) G = g2;
+  }
   if (G > a.ntaps) G = a.ntaps;
   p.G = G;
   p.ngroups = (a.ntaps + G - 1) / G;
