@@ -236,7 +236,11 @@ def main(argv=None):
     parser.add_argument("--lambda", type=float, default=0.0067, dest="lmbda", help="Lambda for rate-distortion tradeoff.")
     parser.add_argument("--tune_iter", type=int, default=100, help="Finetune Iteration")
     parser.add_argument("--arch", default="net_ga", choices=["net_ga", "net_unet_ha_hs"])
-    parser.add_argument("--precision", default="fp32", choices=["fp32", "fp16"])
+    parser.add_argument("--precision", default="fp32", choices=["fp32", "fp32x6", "fp32x3", "bf16", "fp16"],
+                        help="fp32: exact fp32 (the reference's arithmetic); fp32x6: fp32 activations and "
+                             "accumulation, products from six bf16 MFMA products of exact three-part splits "
+                             "(fp32 grade, faster); fp32x3: fp16-part products (~22 bits, not fp32 grade); "
+                             "bf16 / fp16: 16-bit activations (not parity grade)")
     parser.add_argument("--all-images", action="store_true", dest="all_images")
     parser.add_argument("--noise_seed", type=int, default=None,
                         help="price y + U(-1/2,1/2) as the reference's eval does (its nets are never put in "

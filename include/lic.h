@@ -475,9 +475,17 @@ int lic_dwconv_wgrad(int32_t dtype, const void* x, int32_t ldx, const void* dz, 
                      int32_t ntaps, const int8_t* dy, const int8_t* dx, float* dw, float* ws,
                      int64_t ws_bytes, lic_stream_t stream);
 
-/* Library info. */
+/* Library info.
+ * LIC_ABI_VERSION changes whenever an entry point's parameter list or an args struct's layout
+ * changes (3: lic_conv_args.mfma_mode / wgt_split, lic_rate_train_* seed_dev / seed_mul).  A
+ * caller compiled against this header checks lic_abi_version() == LIC_ABI_VERSION and
+ * lic_args_size(k) == sizeof(...) once after loading the library (the Python host does, _ffi.load). */
+#define LIC_ABI_VERSION 3
+enum { LIC_ARGS_CONV = 0, LIC_ARGS_ATTN = 1, LIC_ARGS_RATE = 2, LIC_ARGS_RANS = 3, LIC_ARGS_WGRAD = 4 };
 const char* lic_last_error(void);
 const char* lic_version(void);
+int32_t lic_abi_version(void);
+int64_t lic_args_size(int32_t which);   /* sizeof the LIC_ARGS_* struct the library was built with, -1 if unknown */
 int lic_device_arch(char* buf, int32_t len);
 
 #ifdef __cplusplus

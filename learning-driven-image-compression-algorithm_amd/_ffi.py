@@ -18,12 +18,14 @@ ACT_NONE, ACT_RELU, ACT_LRELU, ACT_GELU, ACT_ROUND = 0, 1, 2, 3, 4
 PRO_NONE, PRO_SQUARE, PRO_ABS = 0, 1, 2
 EPI_PLAIN, EPI_GATE, EPI_HALF_TANH, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, EPI_RES_ACT = 0, 1, 2, 3, 4, 5, 6
 MAX_TAPS = 64
+ABI_VERSION = 3   # include/lic.h LIC_ABI_VERSION
 
 EXPORTED_SYMBOLS = (
     "lic_conv2d_fwd", "lic_gdn_prepare", "lic_win_attn_fwd", "lic_layernorm_fwd",
     "lic_gauss_rate_fwd", "lic_quantize_median", "lic_bpp_finalize", "lic_syntax_recon_fwd",
     "lic_psnr_finalize", "lic_nchw_to_nhwc", "lic_nhwc_to_nchw", "lic_add", "lic_copy",
-    "lic_avgpool", "lic_rb3_fwd", "lic_last_error", "lic_version", "lic_device_arch",
+    "lic_avgpool", "lic_rb3_fwd", "lic_last_error", "lic_version", "lic_abi_version", "lic_args_size",
+    "lic_device_arch",
     "lic_gauss_pmf", "lic_eb_pmf", "lic_pmf_to_cdf", "lic_gauss_indexes", "lic_quantize_symbols",
     "lic_rans_cap", "lic_rans_encode", "lic_rans_pack", "lic_rans_decode",
     "lic_pool_partials", "lic_ca_apply_fwd", "lic_lam_parts", "lic_lam_fwd", "lic_csam_fwd", "lic_recon_fwd",
@@ -223,6 +225,18 @@ def load():
         getattr(lib, name).restype = ctypes.c_int32
     lib.lic_last_error.restype = ctypes.c_char_p
     lib.lic_version.restype = ctypes.c_char_p
+    lib.lic_abi_version.restype = ctypes.c_int32
+    lib.lic_args_size.argtypes = [I]
+    lib.lic_args_size.restype = ctypes.c_int64
+    abi = lib.lic_abi_version()
+    if abi != ABI_VERSION:
+        _load_error = f"liblic ABI {abi} at {path}, this host expects {ABI_VERSION}: rebuild liblic.so"
+        raise LicError(_load_error)
+    for which, st in enumerate((ConvArgs, AttnArgs, RateArgs, RansArgs, WgradArgs)):
+        if lib.lic_args_size(which) != ctypes.sizeof(st):
+            _load_error = (f"liblic args struct {st.__name__}: library {lib.lic_args_size(which)} bytes, "
+                           f"host {ctypes.sizeof(st)}: rebuild liblic.so")
+            raise LicError(_load_error)
     _lib = lib
     return lib
 
@@ -233,7 +247,9 @@ _SYNC_EACH = os.environ.get("LIC_SYNC_EACH", "") not in ("", "0")   # debugging 
 def check(status: int):
     if _SYNC_EACH:
         import torch
-        torch.cuda.synchronize()
+        # a device sync is illegal while a hipGraph is being captured: skip it there
+        if not torch.cuda.is_current_stream_capturing():
+            torch.cuda.synchronize()
     if status != 0:
         msg = _lib.lic_last_error().decode() if _lib is not None else "unknown"
         raise LicError(msg)

@@ -29,7 +29,18 @@ hipError_t ensure_dyn_lds(const void* kern, int bytes) {
 }  // namespace lic
 
 extern "C" const char* lic_last_error(void) { return lic::g_err.c_str(); }
-extern "C" const char* lic_version(void) { return "liblic 0.1 gfx950"; }
+extern "C" const char* lic_version(void) { return "liblic 0.3 gfx950 (abi 3)"; }
+extern "C" int32_t lic_abi_version(void) { return LIC_ABI_VERSION; }
+extern "C" int64_t lic_args_size(int32_t which) {
+  switch (which) {
+    case LIC_ARGS_CONV: return (int64_t)sizeof(lic_conv_args);
+    case LIC_ARGS_ATTN: return (int64_t)sizeof(lic_attn_args);
+    case LIC_ARGS_RATE: return (int64_t)sizeof(lic_rate_args);
+    case LIC_ARGS_RANS: return (int64_t)sizeof(lic_rans_args);
+    case LIC_ARGS_WGRAD: return (int64_t)sizeof(lic_wgrad_args);
+    default: return -1;
+  }
+}
 extern "C" int lic_device_arch(char* buf, int32_t len) {
   hipDeviceProp_t p;
   int dev = 0;

@@ -3,21 +3,7 @@
 // The spatial-tile conv of conv_halo.h for fp32 activations, with every product formed from
 // 16-bit parts on v_mfma_f32_32x32x16_{f16,bf16} instead of the 16x slower fp32-input MFMA.
 //
-// mfma_mode 2, "fp32x6" (bf16 parts, fp32 grade):
-//   x = x0 + x1 + x2, x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)   (split in LDS)
-//   w = w0 + w1 + w2 likewise                                                  (packed on the host)
-//   x * w ~= x0w0 + x0w1 + x1w0 + x0w2 + x1w1 + x2w0                           (one fp32 accumulator)
-// bf16 keeps fp32's exponent range and three RNE parts carry all 24 significand bits, so the
-// splits are exact (no scaling, no subnormal loss); the dropped terms x1w2 + x2w1 + x2w2 are
-// <= 2^-26 |x w|, below the fp32 rounding of the accumulation itself (2^-24).
-//
-// mfma_mode 1, "fp32x3" (fp16 parts, ~3e-7 per product):
-//   x: x_hi = fp16(x),  x_lo = fp16(x - x_hi)
-//   w: W1 = fp16(w) * 2^11 (exact),  W2 = fp16((w - fp16(w)) * 2^11)
-//   2^11 * x * w ~= x_hi*W1 + x_hi*W2 + x_lo*W1, the accumulator scaled by 2^-11 in the epilogue.
-// The dropped term (x - x_hi)(w - fp16(w)) is <= 2^-22 |x w| and each part carries 11 bits, so
-// a product is within ~3e-7 of its fp32 value (fp32 itself: 6e-8).  x_lo is an fp16 subnormal
-// for |x| < 2^-3; its absolute error stays <= 2^-25.
+// Split modes and the packed-weight layout: conv_split.h.
 //
 // Per 16-channel chunk the fp32 halo of the tile arrives by LDS-DMA in a staging buffer
 // (double-buffered, the next chunk's DMA overlaps this chunk's MFMAs); all threads then
@@ -25,10 +11,9 @@
 // halves XOR-swizzled), and every tap reads its shifted windows from the planes.  Weights
 // stream as [G taps][BN][NPB planes x 32 B] stages by LDS-DMA (double buffer).
 #include "conv_halo.h"
+#include "conv_split.h"
 
 namespace lic {
-
-constexpr float kSplitScale = 2048.0f;  // 2^11 (mode 1)
 
 // SPLIT_PARTIAL: chain the products of one tap from zero and add the partial to the running sum
 // with an fp32 VALU add (else the running sum is the MFMA's C operand).  SPLIT_ALT: odd channel
@@ -42,20 +27,15 @@ constexpr float kSplitScale = 2048.0f;  // 2^11 (mode 1)
 #ifndef SPLIT_SMALL_2WG
 #define SPLIT_SMALL_2WG 1
 #endif
-
-template <int MODE> struct SplitMode;
-template <> struct SplitMode<1> {   // fp16: x_hi, x_lo x W1, W2
-  using T = half_t;
-  static constexpr int NPA = 2, NPB = 2, NPROD = 3;
-  static constexpr int PA[NPROD] = {0, 0, 1}, PB[NPROD] = {0, 1, 0};
-  static constexpr float scale = 1.0f / kSplitScale;
-};
-template <> struct SplitMode<2> {   // bf16: x0, x1, x2 x w0, w1, w2
-  using T = bf16_t;
-  static constexpr int NPA = 3, NPB = 3, NPROD = 6;
-  static constexpr int PA[NPROD] = {0, 0, 1, 0, 1, 2}, PB[NPROD] = {0, 1, 0, 2, 1, 0};
-  static constexpr float scale = 1.0f;
-};
+// diagnostic ablations (-DSPLIT_ABL=bits, timing only; outputs are wrong): 1 no in-loop LDS-DMA,
+// 2 no epilogue, 4 no split pass, 8 no MFMA (one VALU op per product group), 16 no fragment reads
+#ifndef SPLIT_ABL
+#define SPLIT_ABL 0
+#endif
+// diagnostic builds: only the fp32x6 16x16x128 / 8x8x64 tiles (fast compile)
+#ifndef SPLIT_DIAG_ONLY
+#define SPLIT_DIAG_ONLY 0
+#endif
 
 template <int MODE, int TH, int TW, int BN, int WM, int WN>
 __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic_conv_args a, const HaloPlan p) {
@@ -139,7 +119,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
       const int row = q / (2 * NPB), slot = q - row * (2 * NPB);
       const int tt = row / BN, n = row - tt * BN;
       const int piece = (slot & ~1) | ((slot & 1) ^ ((n >> 3) & 1));
-      const T* src = wg + ((int64_t)(n0 + n) * a.ntaps + t0 + tt) * (NPB * a.cpad) + k * (16 * NPB) + piece * 8;
+      const int ng = n0 + n;   // fragment-order pack (conv_split.h): part piece>>1, lane (ng&31) + 32*(piece&1)
+      const T* src = wg + split_frag_off(ng >> 5, k, t0 + tt, piece >> 1, nchunks, a.ntaps, NPB) +
+                     ((ng & 31) + 32 * (piece & 1)) * 8;
       glds16(src, dst + q0 * 16);
     }
   };
@@ -150,24 +132,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
   auto split_chunk = [&](int buf, bool neg) {
     const char* src = stg0 + buf * sbytes;
     const float sg = neg ? -1.f : 1.f;
-    const int pro = a.prologue;
     for (int q = tid; q < hq_total; q += NT) {
       const int hp = q >> 2, c = q & 3;
-      float4 v = *(const float4*)(src + q * 16);
-      if (pro == LIC_PRO_SQUARE) v = make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
-      else if (pro == LIC_PRO_ABS) v = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
-      float r[4] = {sg * v.x, sg * v.y, sg * v.z, sg * v.w};
+      uint2 parts[NPA];
+      split4<MODE>(*(const float4*)(src + q * 16), a.prologue, sg, parts);
       const int off = hp * 32 + (((c >> 1) ^ ((hp >> 3) & 1)) << 4) + (c & 1) * 8;
 #pragma unroll
-      for (int pl = 0; pl < NPA; ++pl) {
-        T part[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          part[e] = (T)r[e];
-          r[e] -= (float)part[e];      // exact: the residual fits fp32
-        }
-        *(uint2*)(pl0 + pl * pbytes + off) = *(const uint2*)part;
-      }
+      for (int pl = 0; pl < NPA; ++pl) *(uint2*)(pl0 + pl * pbytes + off) = parts[pl];
     }
   };
 
@@ -204,19 +175,26 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = -acc[i][j];
 #endif
+#if !(SPLIT_ABL & 4)
       split_chunk(k & 1, SPLIT_ALT && (k & 1));
+#endif
       __syncthreads();
     }
     constexpr int NL = HALO_LOADERS < NT / 64 ? HALO_LOADERS : NT / 64;
+#if !(SPLIT_ABL & 1)
     if (wave < NL) {
       if (s + 1 < nst) issue_w(s + 1, (s + 1) & 1, NL);
       if (g == 0 && k + 1 < nchunks) issue_halo(k + 1, (k + 1) & 1, NL);
     }
+#endif
     const char* wb = wbuf0 + (s & 1) * wbytes;
     const int t0 = g * p.G;
     const int gcur = min(p.G, a.ntaps - t0);
     int cy = t0 / p.nx, cx = t0 - cy * p.nx;
     auto load_frags = [&](int tt, u32x4(&fa)[NPA][TM], u32x4(&fb)[NPB][TN]) {
+#if SPLIT_ABL & 16
+      if (tt > 0) return;
+#endif
       const int toff = p.toff0 + cy * p.ystep + cx * p.xstep;
       if (++cx == p.nx) {
         cx = 0;
@@ -248,7 +226,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-#if SPLIT_PARTIAL
+#if SPLIT_ABL & 8
+          acc[i][j][0] += __int_as_float(fa[0][i][0] ^ fa[NPA - 1][i][1] ^ fb[0][j][0] ^ fb[NPB - 1][j][1]);
+#elif SPLIT_PARTIAL
           floatx16 t = mfma_k16<T>(fa[SM::PA[SM::NPROD - 1]][i], fb[SM::PB[SM::NPROD - 1]][j], floatx16{});
 #pragma unroll
           for (int pr = SM::NPROD - 2; pr >= 0; --pr)   // smallest terms first
@@ -278,6 +258,19 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
   }
 
   // with SPLIT_ALT and the running sum as C, an even chunk count leaves it negated
+#if SPLIT_ABL & 2
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z += acc[i][j][r];
+    if (z == 1234.5f) ((float*)a.y)[tid] = z;
+    return;
+  }
+#endif
   const float oscale = (!SPLIT_PARTIAL && SPLIT_ALT && nchunks > 0 && !(nchunks & 1)) ? -SM::scale : SM::scale;
   float* ct = (float*)smem + wave * (32 * 33);
   epilogue_all<float, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, [&](int q) {
@@ -364,6 +357,11 @@ static int split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
   };
   // each try returns 0 without launching when its LDS plan does not fit (e.g. stride-2 halos)
+#if SPLIT_DIAG_ONLY
+  if (MODE == 2 && a.copad % 64 == 0 && a.mi > 8 && try_halo_split<2, 16, 16, 64, 4, 2>(a, s, status)) return 1;
+  if (MODE == 2 && a.copad % 64 == 0 && try_halo_split<2, 8, 8, 64, 2, 2>(a, s, status)) return 1;
+  return 0;
+#else
   if (a.mi > 8 && a.mj > 8) {
     // 16x16 x 192 (8 waves of 64 px x 96 ch) fits the fp32x3 fragments in 256 VGPRs; a 4-wave
     // 128 px x 96 ch variant (acc in AGPRs, 1 wave per SIMD) measured 23 % slower
@@ -382,6 +380,7 @@ static int split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     return 1;
   if (a.copad % 64 == 0 && blocks(8, 8, 64) >= 128 && try_halo_split<MODE, 8, 8, 64, 2, 2>(a, s, status)) return 1;
   return 0;
+#endif
 }
 
 // Returns 1 and launches when a split tile config applies (fp32, mfma_mode 1 / 2, k x k taps incl. 1x1),

@@ -1,0 +1,340 @@
+// fp32 convolutions on the 16-bit matrix cores, "weights-direct" form (lic_conv_args.mfma_mode 2
+// fp32x6 / 1 fp32x3; split arithmetic and packed-weight layout: conv_split.h).
+//
+// Why a second split kernel.  conv_halo_split.hip stages everything through LDS behind one
+// workgroup-wide barrier per weight stage (LDS-DMA of the fp32 halo and of [G taps][BN][parts]
+// weight stages, a split pass between barriers, one 160 KB workgroup per CU): on gfx950 the
+// fp32x6 3x3 192->192 conv at 64^2 spent 495 us against 300 us for its bare MFMA stream
+// (ablations, profiles/r03/split_ablation.txt: DMA 75 us, split 42, fragment reads 27, epilogue 25,
+// none of it overlapped with MFMAs).  Here:
+//   * weights never touch LDS: they are packed in MFMA-fragment order, so each wave loads its B
+//     fragments for the next (chunk, tap) step straight from L2 into VGPRs (one contiguous 1 KB
+//     global_load_dwordx4 per fragment) while the current step's MFMAs run -- no weight barrier;
+//   * the fp32 halo of the NEXT chunk is prefetched into registers (16 B per thread and quad) a
+//     whole chunk ahead, split in registers and written to the other of two LDS plane sets
+//     after the current chunk's taps: ONE barrier per 16-channel chunk;
+//   * the LDS footprint (two plane sets of the halo, 16 bits x parts) fits two workgroups per CU,
+//     so one workgroup's split / barrier / epilogue overlaps the other's MFMAs.
+// Per wave and step: TM x NPA fragment reads from LDS (ds_read_b128) and TN x NPB 1 KB weight
+// loads for NPROD x TM x TN MFMAs (fp32x6, TM = 4, TN = 1: 12 reads + 3 loads per 24 MFMAs).
+#include "conv_halo.h"
+#include "conv_split.h"
+#include <type_traits>
+
+// odd channel chunks are split from -x and the running sum flips sign at every chunk start: the
+// 16-bit MFMA's accumulation rounding is biased toward -inf and the two halves cancel
+#ifndef WD_ALT
+#define WD_ALT 1
+#endif
+
+namespace lic {
+
+struct WdPlan {
+  int hh, hw, hpix;          // halo rows, cols, pixels
+  int plane_bytes, set_bytes;// one 16-bit plane (32 B per halo pixel), NPA planes
+  int dbuf;                  // two plane sets (one barrier per chunk) or one (two)
+  int tiles_y, tiles_x;
+  int toff0, nx, ystep, xstep;  // tap grid: tap t at halo offset toff0 + (t/nx)*ystep + (t%nx)*xstep
+  int dymin, dxmin;
+  int rp_off;                // byte offset of rowpix[BM] + bias[BN]
+  int nchunks;
+};
+
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ>
+__global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const lic_conv_args a, const WdPlan p) {
+  using SM = SplitMode<MODE>;
+  using T = typename SM::T;
+  constexpr int NPA = SM::NPA, NPB = SM::NPB, NPROD = SM::NPROD;
+  constexpr int NT = WM * WN * 64;
+  constexpr int BM = TH * TW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  // chunks unrolled per loop trip so that the B-ring slot of every step is a compile-time index
+  constexpr int KU = (NTAPS % 3 == 0) ? 1 : 3;
+  static_assert(WTM % 32 == 0 && WTN % 32 == 0 && NT % 4 == 0, "tile");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* rowpix = (int*)(smem + p.rp_off);
+  float* sbias = (float*)(rowpix + BM);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lrow = lane & 31, lhalf = lane >> 5;
+
+  int bid = blockIdx.x;
+  const int tx_t = bid % p.tiles_x;
+  bid /= p.tiles_x;
+  const int ty_t = bid % p.tiles_y;
+  const int b = bid / p.tiles_y;
+  const int n0 = blockIdx.y * BN;
+  const int i0 = ty_t * TH, j0 = tx_t * TW;
+  const int iy0 = i0 * a.isy + p.dymin, ix0 = j0 * a.isx + p.dxmin;
+
+  for (int n = tid; n < BN; n += NT) sbias[n] = (a.bias && n0 + n < a.co) ? a.bias[n0 + n] : 0.f;
+  for (int m = tid; m < BM; m += NT) {
+    const int i = i0 + m / TW, j = j0 + m % TW;
+    int base = -1;
+    if (i < a.mi && j < a.mj) {
+      int oy = a.oy0 + a.osy * i, ox = a.ox0 + a.osx * j;
+      if (a.out_shuffle >= 2) { oy *= 2; ox *= 2; }
+      base = (b * a.ho + oy) * a.wo + ox;
+    }
+    rowpix[m] = base;
+  }
+
+  const float* __restrict__ xg = (const float*)a.x;
+  const int nchunks = p.nchunks;
+  const int nsteps = nchunks * NTAPS;
+  const int pro = a.prologue;
+
+  // Every load below is unconditional (clamped indices, zero-selects): a load under a branch makes
+  // the compiler's wait-count merge assume it was skipped, and the next wait then drains the whole
+  // in-order vmcnt queue -- each step would wait for its own prefetch.
+  // halo quads of this thread: pixel hp = (tid >> 2) + i * NT/4, channels 4c4 .. 4c4+3 of the chunk
+  const int c4 = tid & 3;
+  int qsrc[NQ];   // element offset of the quad's pixel in x (channel 4c4 of chunk 0), -1 = zero / none
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int hp = (tid >> 2) + i * (NT / 4);
+    const int r = hp / p.hw, cc = hp - r * p.hw;
+    const int iy = iy0 + r, ix = ix0 + cc;
+    const bool ok = hp < p.hpix && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    qsrc[i] = ok ? ((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4 : -1;
+  }
+  // raw buffer loads: an out-of-range offset reads zeros (padding / out-of-image pixels) with no
+  // branch and no select the compiler could turn back into a conditional load
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)xg, (short)0, (int)((int64_t)a.n * a.h * a.w * a.ldx * 4), 0x00020000);
+  u32x4 hreg[NQ];
+  auto load_halo = [&](int k) {
+    const int c0 = k * 16;
+    const bool cok = c0 + c4 * 4 < a.ci;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const unsigned off = (qsrc[i] >= 0 && cok) ? (unsigned)(qsrc[i] + c0) * 4u : 0x80000000u;
+      hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
+    }
+  };
+  // every quad stores (plane_bytes covers NQ * NT/4 pixels): no per-lane branch around the stores
+  auto split_store = [&](int k, char* set) {
+    const float sg = (WD_ALT && (k & 1)) ? -1.f : 1.f;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int hp = (tid >> 2) + i * (NT / 4);
+      uint2 parts[NPA];
+      const u32x4 h = hreg[i];
+      split4<MODE>(make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w)),
+                   pro, sg, parts);
+      const int off = hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
+#pragma unroll
+      for (int pl = 0; pl < NPA; ++pl) *(uint2*)(set + pl * p.plane_bytes + off) = parts[pl];
+    }
+  };
+
+  int hbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mm = wm * WTM + i * 32 + lrow;
+    const int ty = mm / TW, tx = mm % TW;
+    hbase[i] = ty * a.isy * p.hw + tx * a.isx;
+  }
+  // part pl of the A fragments of the tap at halo offset `toff` (scalar tap cursor, see chunk)
+  auto load_a_part = [&](const char* set, int toff, int pl, u32x4(&fa)[NPA][TM]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int hp = hbase[i] + toff;
+      const int o = hp * 32 + ((lhalf ^ ((hp >> 3) & 1)) << 4);
+      fa[pl][i] = *(const u32x4*)(set + pl * p.plane_bytes + o);
+    }
+  };
+  // B fragments of step s = chunk * NTAPS + tap (clamped): n-tile (n0/32 + wn*TN + j), 1 KB per part
+  const T* __restrict__ wlane = (const T*)a.wgt_split + (int64_t)(n0 / 32 + wn * TN) * nsteps * NPB * 512 + lane * 8;
+  auto load_b = [&](int s, u32x4(&fb)[NPB][TN]) {
+    s = s < nsteps ? s : nsteps - 1;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < NPB; ++pl)
+        fb[pl][j] = *(const u32x4*)(wlane + ((int64_t)j * nsteps + s) * (NPB * 512) + pl * 512);
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // A: ONE register set; each part is re-read for the next tap right after this tap's last product
+  // that reads it (products run smallest first, pr = NPROD-1 .. 0, so part NPA-1 is free after the
+  // first group and part 0 is needed first only by the third), so the reads have most of a step
+  // to land.  B: a ring of three by step, B(s+2) issued at step s.
+  u32x4 fa[NPA][TM], fb[3][NPB][TN];
+  // one tap's products; the running sum is the MFMA's C operand
+  auto step = [&](const char* set, int toff_next, bool has_next, const u32x4(&fbc)[NPB][TN]) {
+#pragma unroll
+    for (int pr = NPROD - 1; pr >= 0; --pr) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_k16<T>(fa[SM::PA[pr]][i], fbc[SM::PB[pr]][j], acc[i][j]);
+      bool last = true;   // the last product of this tap reading part PA[pr] (folded at compile time)
+#pragma unroll
+      for (int q = 0; q < pr; ++q) last = last && SM::PA[q] != SM::PA[pr];
+      if (has_next && last) load_a_part(set, toff_next, SM::PA[pr], fa);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  load_halo(0);
+  split_store(0, smem);
+  load_halo(1 < nchunks ? 1 : 0);
+  load_b(0, fb[0]);
+  load_b(1, fb[1]);
+  __syncthreads();
+
+  // one chunk; KS = chunk index mod KU (compile-time), so step s = k*NTAPS + t sits in ring slot
+  // (KS*NTAPS + t) % 3
+  auto chunk = [&](int k, auto ks) {
+    constexpr int KS = decltype(ks)::value;
+    const char* set = smem + (p.dbuf ? (k & 1) * p.set_bytes : 0);
+#if WD_ALT
+    if (k > 0)   // exact sign flip: the running sum changes sign with the chunk's parts
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = -acc[i][j];
+#endif
+    int toff = p.toff0, cx = 0;   // tap grid cursor (scalar)
+#pragma unroll
+    for (int pl = 0; pl < NPA; ++pl) load_a_part(set, toff, pl, fa);
+#pragma unroll
+    for (int t = 0; t < NTAPS; ++t) {
+      const int sr = KS * NTAPS + t;
+      // kept in this order by the scheduling barriers: the prefetches are issued before this
+      // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
+      load_b(k * NTAPS + t + 2, fb[(sr + 2) % 3]);
+      if (t + 1 < NTAPS) {
+        toff += p.xstep;
+        if (++cx == p.nx) {
+          cx = 0;
+          toff += p.ystep - p.nx * p.xstep;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      step(set, toff, t + 1 < NTAPS, fb[sr % 3]);
+    }
+    // next chunk's parts into the other set (after the last chunk: a harmless duplicate), and the
+    // one after it into the prefetch registers
+    if (!p.dbuf) __syncthreads();   // one plane set: every wave is past this chunk's reads
+    split_store(k + 1, smem + (p.dbuf ? ((k + 1) & 1) * p.set_bytes : 0));
+    load_halo(k + 2 < nchunks ? k + 2 : nchunks - 1);
+    __syncthreads();
+  };
+  for (int k = 0; k < nchunks; k += KU) {
+    chunk(k, std::integral_constant<int, 0>{});
+    if constexpr (KU == 3) {
+      if (k + 1 >= nchunks) break;
+      chunk(k + 1, std::integral_constant<int, 1>{});
+      if (k + 2 >= nchunks) break;
+      chunk(k + 2, std::integral_constant<int, 2>{});
+    }
+  }
+
+  // with WD_ALT an even chunk count leaves the running sum negated
+  const float oscale = (WD_ALT && nchunks > 0 && !(nchunks & 1)) ? -SM::scale : SM::scale;
+  float* ct = (float*)smem + wave * (32 * 33);
+  auto stage = [&](int q) {
+#pragma unroll
+    for (int qq = 0; qq < TM * TN; ++qq)
+      if (qq == q) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * oscale;
+      }
+  };
+  epilogue_all<float, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, stage);
+}
+
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ>
+static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int NPA = SplitMode<MODE>::NPA;
+  if (a.ntaps != NTAPS || a.copad % BN || a.cpad % 16 || a.ci % 4 || a.ldx % 4 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt_split % 16))
+    return 0;
+  if ((int64_t)a.n * a.h * a.w * a.ldx >= (1LL << 31)) return 0;
+  WdPlan p;
+  int dymin = 1 << 20, dymax = -(1 << 20), dxmin = 1 << 20, dxmax = -(1 << 20);
+  for (int t = 0; t < a.ntaps; ++t) {
+    dymin = dymin < a.dy[t] ? dymin : a.dy[t];
+    dymax = dymax > a.dy[t] ? dymax : a.dy[t];
+    dxmin = dxmin < a.dx[t] ? dxmin : a.dx[t];
+    dxmax = dxmax > a.dx[t] ? dxmax : a.dx[t];
+  }
+  p.dymin = dymin;
+  p.dxmin = dxmin;
+  p.hh = (TH - 1) * a.isy + (dymax - dymin) + 1;
+  p.hw = (TW - 1) * a.isx + (dxmax - dxmin) + 1;
+  p.hpix = p.hh * p.hw;
+  if ((p.hpix + NT / 4 - 1) / (NT / 4) > NQ) return 0;     // the halo needs more quads per thread
+  if ((int64_t)a.n * a.h * a.w * a.ldx * 4 >= (1LL << 31)) return 0;   // buffer-load byte offsets
+  p.plane_bytes = NQ * (NT / 4) * 32;   // every quad's pixel, valid or not (unconditional stores)
+  p.set_bytes = NPA * p.plane_bytes;
+  int nx = 1;
+  while (nx < a.ntaps && a.dy[nx] == a.dy[0]) ++nx;
+  if (a.ntaps % nx) return 0;
+  const int sy = a.ntaps > nx ? a.dy[nx] - a.dy[0] : 0;
+  const int sx = nx > 1 ? a.dx[1] - a.dx[0] : 0;
+  for (int t = 0; t < a.ntaps; ++t)
+    if (a.dy[t] != a.dy[0] + (t / nx) * sy || a.dx[t] != a.dx[0] + (t % nx) * sx) return 0;
+  p.toff0 = (a.dy[0] - dymin) * p.hw + (a.dx[0] - dxmin);
+  p.nx = nx;
+  p.ystep = sy * p.hw;
+  p.xstep = sx;
+  p.tiles_y = (a.mi + TH - 1) / TH;
+  p.tiles_x = (a.mj + TW - 1) / TW;
+  p.nchunks = a.cpad / 16;
+  const int tail = TH * TW * 4 + BN * 4;
+  const int epi_bytes = (NT / 64) * 32 * 33 * 4;
+  // LDS plan: two plane sets when two workgroups still fit a CU, else one set at two per CU,
+  // else the single-workgroup plans
+  auto need = [&](int sets) { return (sets * p.set_bytes > epi_bytes ? sets * p.set_bytes : epi_bytes) + tail; };
+  if (need(2) <= 80 * 1024) p.dbuf = 1;
+  else if (need(1) <= 80 * 1024) p.dbuf = 0;
+  else if (need(2) <= 160 * 1024) p.dbuf = 1;
+  else if (need(1) <= 160 * 1024) p.dbuf = 0;
+  else return 0;
+  const int sets_bytes = (p.dbuf ? 2 : 1) * p.set_bytes;
+  p.rp_off = sets_bytes > epi_bytes ? sets_bytes : epi_bytes;
+  const int smem = p.rp_off + tail;
+  const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
+  dim3 grid((unsigned)blocks, a.copad / BN);
+  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ>;
+  const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
+  if (ea != hipSuccess) {
+    status = fail(std::string("split wd conv: dynamic LDS attribute: ") + hipGetErrorString(ea));
+    return 1;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(NT), smem, s, a, p);
+  hipError_t e = hipGetLastError();
+  status = e == hipSuccess ? 0 : fail(std::string("split wd conv launch: ") + hipGetErrorString(e));
+  return 1;
+}
+
+// Returns 1 and launches when a weights-direct tile applies, 0 to let the caller try the
+// LDS-staged split kernel (conv_halo_split.hip) or the exact-fp32 kernels.
+int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
+  if (a.mfma_mode != 2 || !a.wgt_split || a.dtype != LIC_F32) return 0;
+  if (a.groups != 1 || a.ntaps < 1 || a.force_direct || a.force_mfma_generic) return 0;
+  if (a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE && a.prologue != LIC_PRO_ABS) return 0;
+  auto blocks = [&](int th, int tw, int bn) {
+    return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
+  };
+  if (a.mi > 8 && a.mj > 8 && a.copad % 64 == 0 && blocks(16, 16, 64) >= 256) {
+    if (try_split_wd<2, 9, 16, 16, 64, 4, 1, 6>(a, s, status)) return 1;
+
+  }
+  return 0;
+}
+
+}  // namespace lic

@@ -8,6 +8,7 @@ synchronise.
 from __future__ import annotations
 
 import ctypes
+import threading
 import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
@@ -266,56 +267,84 @@ def _ptr(a: Optional[Act]):
 # fp32 convolutions on the 16-bit matrix cores (lic_conv_args.mfma_mode, conv_halo_split.hip):
 # mode 2 ("fp32x6": three bf16 parts per operand, six products, fp32 grade) while a Net with
 # precision='fp32x6' runs, mode 1 ("fp32x3": fp16 parts, three products) for 'fp32x3', 0 otherwise.
-_SPLIT_F32 = [0]
+# The mode is per host thread: two threads running Nets of different precisions never see each
+# other's setting (tests/test_gpu_threads.py).
+_SPLIT_TLS = threading.local()
 SPLIT_MODES = {"fp32x3": 1, "fp32x6": 2}
+
+
+def split_mode() -> int:
+    """The calling thread's split MFMA mode (0 = exact fp32 products)."""
+    return getattr(_SPLIT_TLS, "mode", 0)
+
+
+def set_split_mode(mode: int) -> None:
+    _SPLIT_TLS.mode = int(mode)
 
 
 class split_f32:
     """Context: fp32 spatial-tile convolutions form their products from 16-bit parts on the
-    fp16 / bf16 MFMA (include/lic.h mfma_mode).  `mode`: 0 off, 1 fp32x3, 2 fp32x6 (True = 1)."""
+    fp16 / bf16 MFMA (include/lic.h mfma_mode).  `mode`: 0 off, 1 fp32x3, 2 fp32x6 (True = 1).
+    Thread-local: it affects only convolutions launched from the thread that entered it."""
 
     def __init__(self, mode=1):
         self.mode = int(mode)
 
     def __enter__(self):
-        self.prev = _SPLIT_F32[0]
-        _SPLIT_F32[0] = self.mode
+        self.prev = split_mode()
+        set_split_mode(self.mode)
         return self
 
     def __exit__(self, *exc):
-        _SPLIT_F32[0] = self.prev
+        set_split_mode(self.prev)
         return False
 
 
+def _frag_order(parts: Sequence[torch.Tensor]) -> torch.Tensor:
+    """[copad][ntaps][cpad] 16-bit parts -> the MFMA-fragment order of csrc/conv_split.h:
+    [copad/32][cpad/16][ntaps][part][64 lanes][8], lane = 32 * (channel half) + (co % 32)."""
+    co, nt, cp = parts[0].shape
+    P = torch.stack(list(parts), 0).view(len(parts), co // 32, 32, nt, cp // 16, 2, 8)
+    return P.permute(1, 4, 3, 0, 5, 2, 6).reshape(co // 32, cp // 16, nt, len(parts), 64, 8)
+
+
+def split_weights_parts(ws: torch.Tensor) -> torch.Tensor:
+    """Inverse of the fragment order: the packed split weights as [part][copad][ntaps][cpad]."""
+    nt16, nch, nt, npart = ws.shape[:4]
+    P = ws.view(nt16, nch, nt, npart, 2, 32, 8).permute(3, 0, 5, 2, 1, 4, 6)
+    return P.reshape(npart, nt16 * 32, nt, nch * 16)
+
+
 def split_weights(pk: ConvPack, mode: int = 1) -> Optional[torch.Tensor]:
-    """The 16-bit split pack of an fp32 ConvPack, cached on the pack:
-    mode 1: fp16 [copad][ntaps][cpad/16][W1 16 | W2 16], W1 = fp16(w) * 2^11,
-            W2 = fp16((w - fp16(w)) * 2^11); None when a weight is too large for W1 (|w| >= 31);
-    mode 2: bf16 [copad][ntaps][cpad/16][w0 16 | w1 16 | w2 16], w = w0 + w1 + w2 exactly
-            (w0 = bf16(w), w1 = bf16(w - w0), w2 = bf16(w - w0 - w1), round to nearest even)."""
+    """The 16-bit split pack of an fp32 ConvPack in MFMA-fragment order (csrc/conv_split.h:
+    [copad/32][cpad/16][ntaps][part][64][8]), cached on the pack:
+    mode 1: fp16 parts W1 = fp16(w) * 2^11, W2 = fp16((w - fp16(w)) * 2^11); None when a weight
+            is too large for W1 (|w| >= 31);
+    mode 2: bf16 parts w0 = bf16(w), w1 = bf16(w - w0), w2 = bf16(w - w0 - w1) (round to nearest
+            even), w = w0 + w1 + w2 exactly."""
     key = "_split%d" % mode
     sw = pk.__dict__.get(key)
     if sw is not None and sw[0] is pk.w and sw[1] == pk.w._version:
         return sw[2]
     w = pk.w
-    if w.dtype != torch.float32 or w.shape[2] % 16:
+    if w.dtype != torch.float32 or w.shape[2] % 16 or w.shape[0] % 32:
         return None
-    co, nt, cp = w.shape
+    if mode == 1 and torch.cuda.is_available() and w.is_cuda and torch.cuda.is_current_stream_capturing():
+        # mode 1's range check reads |w|max on the host: not possible inside a capture
+        raise _ffi.LicError("split_weights: fp32x3 weight split first needed inside a hipGraph capture; "
+                            "run one eager forward before capturing")
     if mode == 2:
         parts, r = [], w
         for _ in range(3):
             q = r.to(torch.bfloat16)
-            parts.append(q.view(co, nt, cp // 16, 16))
+            parts.append(q)
             r = r - q.float()
-        out = torch.cat(parts, -1).reshape(co, nt, 3 * cp).contiguous()
+        out = _frag_order(parts)
     elif float(w.abs().max()) >= 31.0:
         out = None
     else:
         hi = w.half()
-        w1 = (hi.float() * 2048.0).half()
-        w2 = ((w - hi.float()) * 2048.0).half()
-        out = torch.cat([w1.view(co, nt, cp // 16, 16), w2.view(co, nt, cp // 16, 16)], -1).reshape(co, nt, 2 * cp)
-        out = out.contiguous()
+        out = _frag_order([(hi.float() * 2048.0).half(), ((w - hi.float()) * 2048.0).half()])
     pk.__dict__[key] = (pk.w, pk.w._version, out)
     return out
 
@@ -368,10 +397,13 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     a.out_shuffle = mode
     a.force_direct = 1 if force_direct else 0
     a.force_mfma_generic = 1 if force_generic else 0
-    if _SPLIT_F32[0] and x.dtype == torch.float32 and pk.groups == 1:
-        ws = split_weights(pk, _SPLIT_F32[0])
+    smode = split_mode()
+    if smode == 1 and prologue == _ffi.PRO_SQUARE:
+        smode = 2   # fp32x3's fp16 parts: x^2 leaves fp16's range from |x| >= 256 (GDN) -> bf16 parts
+    if smode and x.dtype == torch.float32 and pk.groups == 1:
+        ws = split_weights(pk, smode)
         if ws is not None:
-            a.mfma_mode, a.wgt_split = _SPLIT_F32[0], _dp(ws)
+            a.mfma_mode, a.wgt_split = smode, _dp(ws)
     check(_lib().lic_conv2d_fwd(ctypes.byref(a), stream_handle()))
     return out
 

@@ -12,7 +12,7 @@ bit-exact (all 256^2 cases measure 0 flips).
 """
 import torch
 
-TIE_EPS = 2e-3      # |frac(y - mu) - 0.5| of a summation-order flip (measured <= 1e-4)
+TIE_EPS = 2e-4      # |frac(y - mu) - 0.5| of a summation-order flip (measured <= 1e-4)
 
 
 def check_symbols(sym_gpu: torch.Tensor, ref: dict, max_rate: float = 3e-5) -> int:

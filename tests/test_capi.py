@@ -30,6 +30,19 @@ def test_library_loads_and_reports_version():
     assert b"gfx950" in lib.lic_version()
 
 
+def test_abi_version_and_struct_sizes():
+    """The loader's ABI gate: the library reports the header's LIC_ABI_VERSION and the sizes
+    of every args struct it was built with, equal to the ctypes layouts."""
+    import ctypes
+    lib = lic_amd.load_library()
+    hdr = (ROOT / "include" / "lic.h").read_text()
+    assert int(re.search(r"#define LIC_ABI_VERSION (\d+)", hdr).group(1)) == _ffi.ABI_VERSION
+    assert lib.lic_abi_version() == _ffi.ABI_VERSION
+    for k, st in enumerate((_ffi.ConvArgs, _ffi.AttnArgs, _ffi.RateArgs, _ffi.RansArgs, _ffi.WgradArgs)):
+        assert lib.lic_args_size(k) == ctypes.sizeof(st), st.__name__
+    assert lib.lic_args_size(99) == -1
+
+
 def test_ctypes_struct_layout_matches_header():
     import ctypes
     # the largest args struct: sizes must agree with the C compiler's layout
@@ -52,7 +65,7 @@ def test_ctypes_struct_offsets_match_c_compiler(tmp_path):
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
     structs = {"lic_conv_args": _ffi.ConvArgs, "lic_attn_args": _ffi.AttnArgs,
-               "lic_rate_args": _ffi.RateArgs, "lic_rans_args": _ffi.RansArgs}
+               "lic_rate_args": _ffi.RateArgs, "lic_rans_args": _ffi.RansArgs, "lic_wgrad_args": _ffi.WgradArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lic.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
