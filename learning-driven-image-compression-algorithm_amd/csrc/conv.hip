@@ -26,6 +26,7 @@ int try_halo(const lic_conv_args& a, hipStream_t s, int& status);
 // fp32 activations on the fp16 matrix cores (mfma_mode 1), conv_halo_split.hip.
 int conv_halo_split_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
 int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
+int conv_split_1x1_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
 
 // Halo tile choice: the largest output-channel block whose grid still fills the
 // chip (>= 200 workgroups of 16x16 pixels), then 8x8-pixel tiles for small maps
@@ -147,6 +148,7 @@ static int conv_dispatch(const lic_conv_args& a, hipStream_t s) {
   if (mfma_ok && !a.force_mfma_generic) {
     int st = 0;
     if constexpr (sizeof(T) == 4) {
+      if (conv_split_1x1_dispatch(a, s, st)) return st;
       if (conv_split_wd_dispatch(a, s, st)) return st;
       if (conv_halo_split_dispatch(a, s, st)) return st;
     }

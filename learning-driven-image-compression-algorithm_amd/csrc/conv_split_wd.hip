@@ -23,6 +23,14 @@
 
 // odd channel chunks are split from -x and the running sum flips sign at every chunk start: the
 // 16-bit MFMA's accumulation rounding is biased toward -inf and the two halves cancel
+// diagnostic ablations (-DWD_ABL=bits, timing only; outputs are wrong): 1 no in-loop split / halo
+// prefetch, 2 no in-loop B loads, 4 no in-loop A reads, 8 no epilogue, 16 no MFMA
+#ifndef WD_ABL
+#define WD_ABL 0
+#endif
+#ifndef WD_SB
+#define WD_SB 0
+#endif
 #ifndef WD_ALT
 #define WD_ALT 1
 #endif
@@ -32,7 +40,7 @@ namespace lic {
 struct WdPlan {
   int hh, hw, hpix;          // halo rows, cols, pixels
   int plane_bytes, set_bytes;// one 16-bit plane (32 B per halo pixel), NPA planes
-  int dbuf;                  // two plane sets (one barrier per chunk) or one (two)
+  int dbuf;                  // two plane sets (always: the next chunk is split during this one)
   int tiles_y, tiles_x;
   int toff0, nx, ystep, xstep;  // tap grid: tap t at halo offset toff0 + (t/nx)*ystep + (t%nx)*xstep
   int dymin, dxmin;
@@ -92,43 +100,38 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   // in-order vmcnt queue -- each step would wait for its own prefetch.
   // halo quads of this thread: pixel hp = (tid >> 2) + i * NT/4, channels 4c4 .. 4c4+3 of the chunk
   const int c4 = tid & 3;
-  int qsrc[NQ];   // element offset of the quad's pixel in x (channel 4c4 of chunk 0), -1 = zero / none
-#pragma unroll
-  for (int i = 0; i < NQ; ++i) {
-    const int hp = (tid >> 2) + i * (NT / 4);
-    const int r = hp / p.hw, cc = hp - r * p.hw;
+  // halo pixel -> (row, col) by a float reciprocal (exact for hp < 2^16 and hw < 2^10)
+  const float inv_hw = 1.0f / (float)p.hw;
+  auto quad_off = [&](int i) -> int {   // element offset of quad i's pixel at channel 4c4, -1 = zero
+    int tv = tid;
+    asm volatile("" : "+v"(tv));   // opaque: recomputed per chunk, not hoisted out of the loop and spilled
+    const int hp = (tv >> 2) + i * (NT / 4);
+    const int r = (int)(((float)hp + 0.5f) * inv_hw), cc = hp - r * p.hw;
     const int iy = iy0 + r, ix = ix0 + cc;
     const bool ok = hp < p.hpix && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-    qsrc[i] = ok ? ((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4 : -1;
-  }
+    return ok ? ((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4 : -1;
+  };
   // raw buffer loads: an out-of-range offset reads zeros (padding / out-of-image pixels) with no
   // branch and no select the compiler could turn back into a conditional load
   const __amdgpu_buffer_rsrc_t xrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)xg, (short)0, (int)((int64_t)a.n * a.h * a.w * a.ldx * 4), 0x00020000);
   u32x4 hreg[NQ];
-  auto load_halo = [&](int k) {
-    const int c0 = k * 16;
-    const bool cok = c0 + c4 * 4 < a.ci;
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const unsigned off = (qsrc[i] >= 0 && cok) ? (unsigned)(qsrc[i] + c0) * 4u : 0x80000000u;
-      hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
-    }
+  auto load_quad = [&](int i, int k) {
+    const int q = quad_off(i);
+    const unsigned off = (q >= 0 && k * 16 + c4 * 4 < a.ci) ? (unsigned)(q + k * 16) * 4u : 0x80000000u;
+    hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
   };
   // every quad stores (plane_bytes covers NQ * NT/4 pixels): no per-lane branch around the stores
-  auto split_store = [&](int k, char* set) {
+  auto split_quad = [&](int i, int k, char* set) {
     const float sg = (WD_ALT && (k & 1)) ? -1.f : 1.f;
+    const int hp = (tid >> 2) + i * (NT / 4);
+    uint2 parts[NPA];
+    const u32x4 h = hreg[i];
+    split4<MODE>(make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w)),
+                 pro, sg, parts);
+    const int off = hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const int hp = (tid >> 2) + i * (NT / 4);
-      uint2 parts[NPA];
-      const u32x4 h = hreg[i];
-      split4<MODE>(make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w)),
-                   pro, sg, parts);
-      const int off = hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
-#pragma unroll
-      for (int pl = 0; pl < NPA; ++pl) *(uint2*)(set + pl * p.plane_bytes + off) = parts[pl];
-    }
+    for (int pl = 0; pl < NPA; ++pl) *(uint2*)(set + pl * p.plane_bytes + off) = parts[pl];
   };
 
   int hbase[TM];
@@ -171,33 +174,56 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   // first group and part 0 is needed first only by the third), so the reads have most of a step
   // to land.  B: a ring of three by step, B(s+2) issued at step s.
   u32x4 fa[NPA][TM], fb[3][NPB][TN];
-  // one tap's products; the running sum is the MFMA's C operand
-  auto step = [&](const char* set, int toff_next, bool has_next, const u32x4(&fbc)[NPB][TN]) {
+  // one tap's products; the running sum is the MFMA's C operand.  `mid` runs after the first product
+  // group: the next chunk's split work of this step, interleaved with the MFMAs by the scheduler
+  auto step = [&](const char* set, int toff_next, bool has_next, const u32x4(&fbc)[NPB][TN], auto&& mid) {
 #pragma unroll
     for (int pr = NPROD - 1; pr >= 0; --pr) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_k16<T>(fa[SM::PA[pr]][i], fbc[SM::PB[pr]][j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) {
+#if WD_ABL & 16
+          acc[i][j][0] += __uint_as_float(fa[SM::PA[pr]][i][0] ^ fbc[SM::PB[pr]][j][0]);
+#else
+          acc[i][j] = mfma_k16<T>(fa[SM::PA[pr]][i], fbc[SM::PB[pr]][j], acc[i][j]);
+#endif
+        }
       bool last = true;   // the last product of this tap reading part PA[pr] (folded at compile time)
 #pragma unroll
       for (int q = 0; q < pr; ++q) last = last && SM::PA[q] != SM::PA[pr];
+#if !(WD_ABL & 4)
       if (has_next && last) load_a_part(set, toff_next, SM::PA[pr], fa);
+#endif
+      if (pr == NPROD - 1) mid();
+#if WD_SB
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
   };
-  load_halo(0);
-  split_store(0, smem);
-  load_halo(1 < nchunks ? 1 : 0);
+  // chunk 0 split up front; chunk 1 in the prefetch registers
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) load_quad(i, 0);
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    split_quad(i, 0, smem);
+    load_quad(i, 1 < nchunks ? 1 : 0);
+  }
   load_b(0, fb[0]);
   load_b(1, fb[1]);
   __syncthreads();
 
   // one chunk; KS = chunk index mod KU (compile-time), so step s = k*NTAPS + t sits in ring slot
-  // (KS*NTAPS + t) % 3
+  // (KS*NTAPS + t) % 3.  During chunk k, step t also splits halo quads [t*QPS, (t+1)*QPS) of chunk
+  // k+1 (in the registers since chunk k-1) into the other plane set -- free since the barrier that
+  // ended chunk k-1 -- and refills those registers with chunk k+2: the split's VALU work and its LDS
+  // stores sit between this wave's MFMAs instead of in a serial phase before the barrier.
+  constexpr int QPS = (NQ + NTAPS - 1) / NTAPS;
   auto chunk = [&](int k, auto ks) {
     constexpr int KS = decltype(ks)::value;
-    const char* set = smem + (p.dbuf ? (k & 1) * p.set_bytes : 0);
+    const char* set = smem + (k & 1) * p.set_bytes;
+    char* nset = smem + ((k + 1) & 1) * p.set_bytes;
+    const int kn = k + 2 < nchunks ? k + 2 : nchunks - 1;
 #if WD_ALT
     if (k > 0)   // exact sign flip: the running sum changes sign with the chunk's parts
 #pragma unroll
@@ -213,7 +239,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
       const int sr = KS * NTAPS + t;
       // kept in this order by the scheduling barriers: the prefetches are issued before this
       // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
+#if !(WD_ABL & 2)
       load_b(k * NTAPS + t + 2, fb[(sr + 2) % 3]);
+#endif
       if (t + 1 < NTAPS) {
         toff += p.xstep;
         if (++cx == p.nx) {
@@ -222,13 +250,21 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-      step(set, toff, t + 1 < NTAPS, fb[sr % 3]);
+      step(set, toff, t + 1 < NTAPS, fb[sr % 3], [&]() {
+#if !(WD_ABL & 1)
+#pragma unroll
+        for (int i = t * QPS; i < (t + 1) * QPS && i < NQ; ++i) {
+          split_quad(i, k + 1, nset);
+#if WD_ABL & 32   // diagnostic: always chunk 0 (L2-resident): separates HBM latency from the split work
+          load_quad(i, 0);
+#else
+          load_quad(i, kn);
+#endif
+        }
+#endif
+      });
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // next chunk's parts into the other set (after the last chunk: a harmless duplicate), and the
-    // one after it into the prefetch registers
-    if (!p.dbuf) __syncthreads();   // one plane set: every wave is past this chunk's reads
-    split_store(k + 1, smem + (p.dbuf ? ((k + 1) & 1) * p.set_bytes : 0));
-    load_halo(k + 2 < nchunks ? k + 2 : nchunks - 1);
     __syncthreads();
   };
   for (int k = 0; k < nchunks; k += KU) {
@@ -243,17 +279,31 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
 
   // with WD_ALT an even chunk count leaves the running sum negated
   const float oscale = (WD_ALT && nchunks > 0 && !(nchunks & 1)) ? -SM::scale : SM::scale;
-  float* ct = (float*)smem + wave * (32 * 33);
-  auto stage = [&](int q) {
+  // every accumulator tile of the wave is staged in LDS first (the plane sets are free after the
+  // last barrier): the accumulators are dead before the epilogue loads its operands
+  constexpr int CTS = 32 * 33;
+  float* ct = (float*)smem + wave * (TM * TN * CTS);
 #pragma unroll
-    for (int qq = 0; qq < TM * TN; ++qq)
-      if (qq == q) {
+  for (int qq = 0; qq < TM * TN; ++qq)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * oscale;
-      }
-  };
-  epilogue_all<float, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, stage);
+    for (int r = 0; r < 16; ++r)
+      ct[qq * CTS + ((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * oscale;
+  auto stage = [&](int) {};
+#if WD_ABL & 8
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z += acc[i][j][r];
+    if (z == 1234.5f) ((float*)a.y)[tid] = z;
+    return;
+  }
+#endif
+  epilogue_all<float, TM * TN, TN, decltype(stage), CTS>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN,
+                                                          lane, stage);
 }
 
 template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ>
@@ -295,15 +345,13 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   p.tiles_x = (a.mj + TW - 1) / TW;
   p.nchunks = a.cpad / 16;
   const int tail = TH * TW * 4 + BN * 4;
-  const int epi_bytes = (NT / 64) * 32 * 33 * 4;
+  constexpr int TQ = (TH * TW / WM / 32) * (BN / WN / 32);   // accumulator tiles per wave
+  const int epi_bytes = (NT / 64) * TQ * 32 * 33 * 4;
   // LDS plan: two plane sets when two workgroups still fit a CU, else one set at two per CU,
   // else the single-workgroup plans
   auto need = [&](int sets) { return (sets * p.set_bytes > epi_bytes ? sets * p.set_bytes : epi_bytes) + tail; };
-  if (need(2) <= 80 * 1024) p.dbuf = 1;
-  else if (need(1) <= 80 * 1024) p.dbuf = 0;
-  else if (need(2) <= 160 * 1024) p.dbuf = 1;
-  else if (need(1) <= 160 * 1024) p.dbuf = 0;
-  else return 0;
+  p.dbuf = 1;   // the next chunk is split during this one: always two plane sets
+  if (need(2) > 160 * 1024) return 0;
   const int sets_bytes = (p.dbuf ? 2 : 1) * p.set_bytes;
   p.rp_off = sets_bytes > epi_bytes ? sets_bytes : epi_bytes;
   const int smem = p.rp_off + tail;
@@ -331,7 +379,7 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
   };
   if (a.mi > 8 && a.mj > 8 && a.copad % 64 == 0 && blocks(16, 16, 64) >= 256) {
-    if (try_split_wd<2, 9, 16, 16, 64, 4, 1, 6>(a, s, status)) return 1;
+    if (try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status)) return 1;
 
   }
   return 0;

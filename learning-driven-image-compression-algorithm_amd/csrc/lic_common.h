@@ -386,15 +386,18 @@ __device__ __forceinline__ void epilogue_tile_scalar(const lic_conv_args& a, con
 // tile q into the wave's private LDS slot ct.  Vector variants finish tiles in
 // pairs with ping-pong operand sets (tile q+1's loads in flight while tile q is
 // finished and stored); MASK < 0 is the scalar path.
-template <typename T, int NQ, int TN, int MASK, typename Stage>
-__device__ __forceinline__ void epilogue_run(const lic_conv_args& a, const float* ct, const int* rowpix_w, int n0_w,
+// CT_STRIDE > 0: tile q is staged at ct + q * CT_STRIDE (all of a wave's tiles staged up front, so the
+// accumulators are dead before the epilogue's operand loads); 0: one slot reused for every tile.
+template <typename T, int NQ, int TN, int MASK, typename Stage, int CT_STRIDE = 0>
+__device__ __forceinline__ void epilogue_run(const lic_conv_args& a, const float* ct0, const int* rowpix_w, int n0_w,
                                              const float* sbias_w, int lane, Stage& stage) {
+  auto ctq = [&](int q) { return ct0 + q * CT_STRIDE; };
   if constexpr (MASK < 0) {
 #pragma nounroll
     for (int q = 0; q < NQ; ++q) {
       stage(q);
       wave_lds_sync();
-      epilogue_tile_scalar<T>(a, ct, rowpix_w + (q / TN) * 32, n0_w + (q % TN) * 32, lane);
+      epilogue_tile_scalar<T>(a, ctq(q), rowpix_w + (q / TN) * 32, n0_w + (q % TN) * 32, lane);
       wave_lds_sync();
     }
   } else {
@@ -402,7 +405,7 @@ __device__ __forceinline__ void epilogue_run(const lic_conv_args& a, const float
     auto tile = [&](int q, const EpiOperands<T>& eo) {
       stage(q);
       wave_lds_sync();
-      epilogue_tile<T, MASK>(a, ct, rowpix_w + (q / TN) * 32, n0_w + (q % TN) * 32, lane, sbias_w + (q % TN) * 32,
+      epilogue_tile<T, MASK>(a, ctq(q), rowpix_w + (q / TN) * 32, n0_w + (q % TN) * 32, lane, sbias_w + (q % TN) * 32,
                              eo);
       wave_lds_sync();
     };
@@ -434,21 +437,27 @@ __device__ __forceinline__ void epilogue_run(const lic_conv_args& a, const float
 }
 
 // Uniform dispatch to the epilogue variant of this launch.
-template <typename T, int NQ, int TN, typename Stage>
+template <typename T, int NQ, int TN, typename Stage, int CT_STRIDE = 0>
 __device__ __forceinline__ void epilogue_all(const lic_conv_args& a, const float* ct, const int* rowpix_w, int n0_w,
                                              const float* sbias_w, int lane, Stage stage) {
   if (!epi_vec_ok<T>(a)) {
-    epilogue_run<T, NQ, TN, -1>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage);
+    epilogue_run<T, NQ, TN, -1, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage);
     return;
   }
   switch (epi_mask(a)) {
-    case 0: epilogue_run<T, NQ, TN, 0>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
-    case EPI_R1: epilogue_run<T, NQ, TN, EPI_R1>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
-    case EPI_G: epilogue_run<T, NQ, TN, EPI_G>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
-    case EPI_G | EPI_R1: epilogue_run<T, NQ, TN, EPI_G | EPI_R1>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
-    case EPI_R2: epilogue_run<T, NQ, TN, EPI_R2>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
-    case EPI_G | EPI_R2: epilogue_run<T, NQ, TN, EPI_G | EPI_R2>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
-    default: epilogue_run<T, NQ, TN, EPI_G | EPI_R1 | EPI_R2>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
+    case 0: epilogue_run<T, NQ, TN, 0, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
+    case EPI_R1: epilogue_run<T, NQ, TN, EPI_R1, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
+    case EPI_G: epilogue_run<T, NQ, TN, EPI_G, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
+    case EPI_G | EPI_R1:
+      epilogue_run<T, NQ, TN, EPI_G | EPI_R1, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage);
+      break;
+    case EPI_R2: epilogue_run<T, NQ, TN, EPI_R2, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage); break;
+    case EPI_G | EPI_R2:
+      epilogue_run<T, NQ, TN, EPI_G | EPI_R2, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage);
+      break;
+    default:
+      epilogue_run<T, NQ, TN, EPI_G | EPI_R1 | EPI_R2, Stage, CT_STRIDE>(a, ct, rowpix_w, n0_w, sbias_w, lane, stage);
+      break;
   }
 }
 

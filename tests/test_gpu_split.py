@@ -29,6 +29,8 @@ DEV = "cuda"
     (192, 576, 1, 1, (0, 0, 0, 0), 32, 64, "plain"),   # 1x1 qkv Linear of Win_noShift_Attention
     (192, 192, 1, 2, (0, 0, 0, 0), 8, 128, "plain"),   # 1x1 s2 skip of ResidualBlockWithStride (8x8 tiles)
     (192, 192, 1, 1, (0, 0, 0, 0), 8, 128, "square"),  # GDN: conv1x1(x^2) (prologue SQUARE)
+    (96, 96, 1, 1, (0, 0, 0, 0), 8, 50, "gate"),       # 1x1 GEMM: ragged M, copad 96 (clamped n-tiles)
+    (192, 192, 1, 1, (0, 0, 0, 0), 8, 64, "gdn"),      # 1x1 GEMM: x^2 prologue + GDN x*rsqrt(n) epilogue
 ])
 def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     import lic_amd.functional as Fn
@@ -38,6 +40,9 @@ def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     m = Conv2d(cin, cout, k, s, 0).to(DEV)
     with torch.no_grad():
         m.bias.normal_(0, 0.1)
+        if epi == "gdn":     # GDN's norm: gamma >= 0, beta > 0 (model/gdn.py) -> sqrt of a positive sum
+            m.weight.abs_()
+            m.bias.abs_().add_(0.5)
     x = torch.randn(B, cin, H, H) * 0.5
     X = Fn.Act.from_nchw(x.to(DEV).contiguous(), torch.float32)
     pk = m.packed(torch.float32, pad)
@@ -45,7 +50,8 @@ def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     r = Fn.Act.from_nchw(torch.randn(B, cout, Ho, Wo).to(DEV), torch.float32)
     g = Fn.Act.from_nchw(torch.rand(B, cout, Ho, Wo).to(DEV), torch.float32)
     kw = {"plain": {}, "gelu": dict(act=L.ACT_GELU), "lrelu_r1": dict(act=L.ACT_LRELU, r1=r),
-          "square": dict(prologue=L.PRO_SQUARE),
+          "square": dict(prologue=L.PRO_SQUARE), "abs": dict(prologue=L.PRO_ABS),
+          "gdn": dict(prologue=L.PRO_SQUARE, epi=L.EPI_GDN_RSQRT, g=g),
           "gate": dict(act=L.ACT_LRELU, epi=L.EPI_GATE, g=g, r2=r, r1=r)}[epi]
     exact = Fn.conv(X, pk, **kw).nchw().cpu()
     with Fn.split_f32(mode):
@@ -59,8 +65,11 @@ def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     base = F.conv2d(F.pad(x, (pad[1], pad[3], pad[0], pad[2])), m.weight.detach().cpu(), m.bias.detach().cpu(), s)
     if epi == "square":
         base = F.conv2d(x * x, m.weight.detach().cpu(), m.bias.detach().cpu(), s)
-    err_cpu = (got - {"plain": base, "gelu": F.gelu(base), "square": base}[epi]).abs().max().item() \
-        if epi in ("plain", "gelu", "square") else 0.0
+    if epi == "abs":
+        base = F.conv2d(F.pad(x.abs(), (pad[1], pad[3], pad[0], pad[2])), m.weight.detach().cpu(),
+                        m.bias.detach().cpu(), s)
+    err_cpu = (got - {"plain": base, "gelu": F.gelu(base), "square": base, "abs": base}[epi]).abs().max().item() \
+        if epi in ("plain", "gelu", "square", "abs") else 0.0
     print(f"\n[split{mode} conv{k}x{k} {cin}->{cout} B={B} {H}^2 {epi}] max err vs exact-fp32 kernel {err:.2e}, "
           f"vs torch {err_cpu:.2e} (scale {scale:.2f})")
     assert not torch.equal(got, exact)          # the split kernel ran
@@ -102,6 +111,11 @@ def test_split_net_parity(arch, B, precision):
     print(f"\n[{arch} {precision} B={B}] bpp {bpp:.8f} ref {ref['bpp'].item():.8f} psnr {psnr:.6f} "
           f"ref {ref['v_psnr'].item():.6f} flips {flips} (exact fp32: {flips0}) y rms err {ez:.2e} (exact fp32: {ez0:.2e})")
     check_symbols(last["symbols"], ref, max_rate=max(3e-5, flips0 / ref["symbols"].numel()))
+    d = ref["z3"] - ref["means"]
+    dist = ((d - torch.floor(d)) - 0.5).abs()
+    diff = flipped ^ res["fp32"][5]
+    print(f"flip-set difference vs exact fp32: {int(diff.sum())} at |frac-1/2| = {dist[diff].tolist()}; "
+          f"all flips: {dist[flipped].tolist()}")
     assert torch.equal(flipped, res["fp32"][5]), "flipped symbols differ from the exact-fp32 path's"
     assert ez <= 1.25 * ez0
     assert abs(bpp - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (B * 65536)

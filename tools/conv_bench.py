@@ -34,6 +34,8 @@ SHAPES = [
     ("ru1x1_128_64@16", 128, 64, 1, 1, (0, 0, 0, 0), 16),
     ("ru1x1_64_128@16", 64, 128, 1, 1, (0, 0, 0, 0), 16),
     ("lin512_128@16", 512, 128, 1, 1, (0, 0, 0, 0), 16),
+    ("proj1x1@64", 192, 192, 1, 1, (0, 0, 0, 0), 64),
+    ("gdn1x1@128", 192, 192, 1, 1, (0, 0, 0, 0), 128),
 ]
 
 

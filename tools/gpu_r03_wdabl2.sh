@@ -1,0 +1,8 @@
+source tools/gpu_step.sh
+mkdir -p gpurun_out/r03wdabl2
+SH=wnsa3x3@64,rbws_conv2@128
+run_step 120 r03wdabl2/abl_base python3 tools/conv_bench.py --dtype fp32x6 --auto-only --iters 30 --only $SH
+for v in noa nob nosplit onlymfma; do
+  LIC_LIB=tools/native/liblic_wd_$v.so run_step 120 r03wdabl2/abl_$v python3 tools/conv_bench.py --dtype fp32x6 --auto-only --iters 30 --only $SH
+done
+echo ALLDONE
