@@ -44,6 +44,8 @@ struct WdPlan {
   int tiles_y, tiles_x;
   int toff0, nx, ystep, xstep;  // tap grid: tap t at halo offset toff0 + (t/nx)*ystep + (t%nx)*xstep
   int dymin, dxmin;
+  int hsy, hsx;              // halo sampling stride: 2 when the launch's taps share one parity at
+                             // input stride 2 (a stride-2 conv's phase, conv.hip), else 1
   int rp_off;                // byte offset of rowpix[BM] + bias[BN]
   int nchunks;
 };
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
     asm volatile("" : "+v"(tv));   // opaque: recomputed per chunk, not hoisted out of the loop and spilled
     const int hp = (tv >> 2) + i * (NT / 4);
     const int r = (int)(((float)hp + 0.5f) * inv_hw), cc = hp - r * p.hw;
-    const int iy = iy0 + r, ix = ix0 + cc;
+    const int iy = iy0 + r * p.hsy, ix = ix0 + cc * p.hsx;
     const bool ok = hp < p.hpix && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
     return ok ? ((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4 : -1;
   };
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   for (int i = 0; i < TM; ++i) {
     const int mm = wm * WTM + i * 32 + lrow;
     const int ty = mm / TW, tx = mm % TW;
-    hbase[i] = ty * a.isy * p.hw + tx * a.isx;
+    hbase[i] = ty * (a.isy / p.hsy) * p.hw + tx * (a.isx / p.hsx);
   }
   // per-chunk opaque copy of hbase: the per-tap fragment addresses are then computed in the chunk,
   // not hoisted out of the chunk loop as NTAPS x TM live registers (which spilled)
@@ -342,8 +344,17 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   }
   p.dymin = dymin;
   p.dxmin = dxmin;
-  p.hh = (TH - 1) * a.isy + (dymax - dymin) + 1;
-  p.hw = (TW - 1) * a.isx + (dxmax - dxmin) + 1;
+  // stride-2 input whose taps all share one row (column) parity: the halo samples every other row
+  // (column) -- the rows of the other parity are never read
+  bool ypar = a.isy == 2, xpar = a.isx == 2;
+  for (int t = 0; t < a.ntaps; ++t) {
+    ypar = ypar && ((a.dy[t] - dymin) & 1) == 0;
+    xpar = xpar && ((a.dx[t] - dxmin) & 1) == 0;
+  }
+  p.hsy = ypar ? 2 : 1;
+  p.hsx = xpar ? 2 : 1;
+  p.hh = ((TH - 1) * a.isy + (dymax - dymin)) / p.hsy + 1;
+  p.hw = ((TW - 1) * a.isx + (dxmax - dxmin)) / p.hsx + 1;
   p.hpix = p.hh * p.hw;
   if ((p.hpix + NT / 4 - 1) / (NT / 4) > NQ) return 0;     // the halo needs more quads per thread
   if ((int64_t)a.n * a.h * a.w * a.ldx * 4 >= (1LL << 31)) return 0;   // buffer-load byte offsets
@@ -356,10 +367,10 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   const int sx = nx > 1 ? a.dx[1] - a.dx[0] : 0;
   for (int t = 0; t < a.ntaps; ++t)
     if (a.dy[t] != a.dy[0] + (t / nx) * sy || a.dx[t] != a.dx[0] + (t % nx) * sx) return 0;
-  p.toff0 = (a.dy[0] - dymin) * p.hw + (a.dx[0] - dxmin);
+  p.toff0 = ((a.dy[0] - dymin) / p.hsy) * p.hw + (a.dx[0] - dxmin) / p.hsx;
   p.nx = nx;
-  p.ystep = sy * p.hw;
-  p.xstep = sx;
+  p.ystep = (sy / p.hsy) * p.hw;
+  p.xstep = sx / p.hsx;
   p.tiles_y = (a.mi + TH - 1) / TH;
   p.tiles_x = (a.mj + TW - 1) / TW;
   p.nchunks = a.cpad / 16;

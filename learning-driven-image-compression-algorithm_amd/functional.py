@@ -349,11 +349,48 @@ def split_weights(pk: ConvPack, mode: int = 1) -> Optional[torch.Tensor]:
     return out
 
 
+def stride2_phase_packs(pk: ConvPack) -> Optional[List[ConvPack]]:
+    """The input-parity phases of a stride-2 k x k ConvPack (k >= 4): four sub-packs holding the taps
+    whose row / column offsets share one parity (5x5: 9, 6, 6 and 4 taps), biased only in the
+    first.  Each phase reads every other input row and column, so the split kernel stages a
+    quarter of the stride-2 halo (conv_split_wd.hip, hsy / hsx); the four launches accumulate into
+    one output (csrc/conv.hip).  Cached on the pack."""
+    if pk.stride != 2 or pk.phase is not None or pk.groups != 1 or min(pk.kh, pk.kw) < 4 or \
+            pk.__dict__.get("_s2phase_of") is not None:
+        return None
+    sub = pk.__dict__.get("_s2phases")
+    if sub is not None and sub[0] is pk.w and sub[1] == pk.w._version:
+        return sub[2]
+    dymin, dxmin = min(pk.dy), min(pk.dx)
+    packs = []
+    for py in (0, 1):
+        for px in (0, 1):
+            idx = [t for t in range(len(pk.dy)) if (pk.dy[t] - dymin) % 2 == py and (pk.dx[t] - dxmin) % 2 == px]
+            packs.append(ConvPack(w=pk.w[:, idx, :].contiguous(), bias=pk.bias if not packs else None, ci=pk.ci,
+                                  co=pk.co, dy=[pk.dy[t] for t in idx], dx=[pk.dx[t] for t in idx],
+                                  groups=1, stride=2, pad=pk.pad, kh=pk.kh, kw=pk.kw))
+            packs[-1].__dict__["_s2phase_of"] = pk
+    pk.__dict__["_s2phases"] = (pk.w, pk.w._version, packs)
+    return packs
+
+
 def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT_NONE, slope: float = 0.01,
          epi: int = _ffi.EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
          y2: Optional[Act] = None, prologue: int = _ffi.PRO_NONE, out_hw=None, shuffle: bool = False,
          force_direct: bool = False, force_generic: bool = False) -> Act:
     """Run one ConvPack launch. For convT phases `out` (full map) must be given."""
+    if (split_mode() == 2 and x.dtype == torch.float32 and not (force_direct or force_generic or shuffle) and
+            act == _ffi.ACT_NONE and epi == _ffi.EPI_PLAIN and r1 is None and g is None and r2 is None and
+            y2 is None and x.B * x.H * x.W >= 65536):
+        phases = stride2_phase_packs(pk)
+        if phases is not None:
+            # fp32x6 stride-2 k x k conv as its four input-parity phases, accumulated in fp32 through
+            # the epilogue's residual operand (the first phase adds the bias)
+            hw = out_hw if out_hw is not None else conv_out_hw(x.H, x.W, pk)
+            out = conv(x, phases[0], out, prologue=prologue, out_hw=hw)
+            for ph in phases[1:]:
+                conv(x, ph, out, r1=out, prologue=prologue, out_hw=hw)
+            return out
     if x.c != pk.ci:
         raise ValueError(f"conv: input has {x.c} channels, weights expect {pk.ci}")
     if pk.w.dtype != x.dtype:

@@ -33,3 +33,25 @@ def test_split_weights_exact_parts():
     err = ((p1.sum(0) / 2048.0 - w).abs() / w.abs().clamp_min(1e-3)).max().item()
     assert err < 1e-6
     assert Fn.split_weights(pk, 2) is ws            # cached on the pack
+
+
+def test_stride2_phase_packs_partition_taps():
+    """ZeroPad2d((1,2,1,2)) + conv5x5 s2 (net_ga.py:277-282): the four parity phases hold 9, 6, 6, 4
+    taps, every tap exactly once, each phase's offsets share one row and one column parity, the
+    bias only in the first; phases are not split again."""
+    pk = Fn.ConvPack.__new__(Fn.ConvPack)
+    dy = [y for y in range(-1, 4) for x in range(-1, 4)]
+    dx = [x for y in range(-1, 4) for x in range(-1, 4)]
+    pk.__dict__.update(w=torch.randn(64, 25, 32), bias=torch.randn(64), ci=32, co=64, dy=dy, dx=dx, groups=1,
+                       stride=2, pad=(1, 1, 2, 2), kh=5, kw=5, phase=None)
+    ph = Fn.stride2_phase_packs(pk)
+    assert [len(p.dy) for p in ph] == [9, 6, 6, 4]
+    seen = sorted((y, x) for p in ph for y, x in zip(p.dy, p.dx))
+    assert seen == sorted(zip(dy, dx))
+    for p in ph:
+        assert len({(y + 1) % 2 for y in p.dy}) == 1 and len({(x + 1) % 2 for x in p.dx}) == 1
+        for t, (y, x) in enumerate(zip(p.dy, p.dx)):
+            assert torch.equal(p.w[:, t], pk.w[:, dy.index(y) * 0 + [i for i in range(25) if dy[i] == y and dx[i] == x][0]])
+    assert ph[0].bias is pk.bias and all(p.bias is None for p in ph[1:])
+    assert Fn.stride2_phase_packs(ph[0]) is None
+    assert Fn.stride2_phase_packs(pk) is ph      # cached
