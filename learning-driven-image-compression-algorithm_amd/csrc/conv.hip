@@ -148,8 +148,8 @@ static int conv_dispatch(const lic_conv_args& a, hipStream_t s) {
   if (mfma_ok && !a.force_mfma_generic) {
     int st = 0;
     if constexpr (sizeof(T) == 4) {
-      if (conv_split_1x1_dispatch(a, s, st)) return st;
       if (conv_split_wd_dispatch(a, s, st)) return st;
+      if (conv_split_1x1_dispatch(a, s, st)) return st;
       if (conv_halo_split_dispatch(a, s, st)) return st;
     }
     if (conv_halo_dispatch<T>(a, s, st)) return st;

@@ -50,7 +50,9 @@ struct WdPlan {
   int nchunks;
 };
 
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ>
+// VT > 0: a 1x1 convolution whose NTAPS = VT "virtual taps" are VT consecutive 16-channel chunks
+// staged together (one barrier per VT chunks; the halo is the tile itself, VT blocks of BM pixels).
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0>
 __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const lic_conv_args a, const WdPlan p) {
   using SM = SplitMode<MODE>;
   using T = typename SM::T;
@@ -63,9 +65,15 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   // B ring: R slots, B(s+2) issued at step s into slot (s+2) % R.  R divides NTAPS where it can (3 or
   // 4), so every chunk starts at slot 0; else the chunk loop is unrolled by KU = 3 (chunk k starts
   // at slot (k*NTAPS) % 3)
-  constexpr int R = (NTAPS % 3 == 0) ? 3 : ((NTAPS % 4 == 0) ? 4 : 3);
+  // (an even tap count that 3 and 4 do not divide: two slots at prefetch distance one)
+  constexpr int R = (NTAPS % 3 == 0) ? 3 : ((NTAPS % 4 == 0) ? 4 : ((NTAPS % 2 == 0) ? 2 : 3));
+  constexpr int PD = R == 2 ? 1 : 2;   // B prefetch distance in steps
   constexpr int KU = (NTAPS % R == 0) ? 1 : 3;
+  constexpr int CSTEP = 16 * (VT > 0 ? VT : 1);   // input channels per chunk
   static_assert(WTM % 32 == 0 && WTN % 32 == 0 && NT % 4 == 0, "tile");
+  static_assert(VT == 0 || VT == NTAPS, "virtual taps");
+  // every accumulator tile staged before the epilogue when that fits the plane sets (TM*TN <= 4)
+  constexpr bool EPI_ALL = TM * TN <= 4;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* rowpix = (int*)(smem + p.rp_off);
@@ -108,14 +116,26 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   const int c4 = tid & 3;
   // halo pixel -> (row, col) by a float reciprocal (exact for hp < 2^16 and hw < 2^10)
   const float inv_hw = 1.0f / (float)p.hw;
-  auto quad_off = [&](int i) -> int {   // element offset of quad i's pixel at channel 4c4, -1 = zero
+  // element offset of quad i's pixel at channel 4c4 (+ its virtual tap's 16-channel block), -1 = zero;
+  // cq = the quad's channel within the chunk
+  auto quad_off = [&](int i, int& cq) -> int {
     int tv = tid;
     asm volatile("" : "+v"(tv));   // opaque: recomputed per chunk, not hoisted out of the loop and spilled
     const int hp = (tv >> 2) + i * (NT / 4);
-    const int r = (int)(((float)hp + 0.5f) * inv_hw), cc = hp - r * p.hw;
-    const int iy = iy0 + r * p.hsy, ix = ix0 + cc * p.hsx;
+    int iy, ix;
+    if constexpr (VT > 0) {
+      const int sub = hp / BM, m = hp - sub * BM;
+      iy = iy0 + (m / TW) * a.isy;
+      ix = ix0 + (m % TW) * a.isx;
+      cq = sub * 16 + c4 * 4;
+    } else {
+      const int r = (int)(((float)hp + 0.5f) * inv_hw), cc = hp - r * p.hw;
+      iy = iy0 + r * p.hsy;
+      ix = ix0 + cc * p.hsx;
+      cq = c4 * 4;
+    }
     const bool ok = hp < p.hpix && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-    return ok ? ((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4 : -1;
+    return ok ? ((b * a.h + iy) * a.w + ix) * a.ldx + cq : -1;
   };
   // raw buffer loads: an out-of-range offset reads zeros (padding / out-of-image pixels) with no
   // branch and no select the compiler could turn back into a conditional load
@@ -123,8 +143,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
       __builtin_amdgcn_make_buffer_rsrc((void*)xg, (short)0, (int)((int64_t)a.n * a.h * a.w * a.ldx * 4), 0x00020000);
   u32x4 hreg[NQ];
   auto load_quad = [&](int i, int k) {
-    const int q = quad_off(i);
-    const unsigned off = (q >= 0 && k * 16 + c4 * 4 < a.ci) ? (unsigned)(q + k * 16) * 4u : 0x80000000u;
+    int cq;
+    const int q = quad_off(i, cq);
+    const unsigned off = (q >= 0 && k * CSTEP + cq < a.ci) ? (unsigned)(q + k * CSTEP) * 4u : 0x80000000u;
     hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
   };
   // every quad stores (plane_bytes covers NQ * NT/4 pixels): no per-lane branch around the stores
@@ -145,7 +166,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
   for (int i = 0; i < TM; ++i) {
     const int mm = wm * WTM + i * 32 + lrow;
     const int ty = mm / TW, tx = mm % TW;
-    hbase[i] = ty * (a.isy / p.hsy) * p.hw + tx * (a.isx / p.hsx);
+    hbase[i] = VT > 0 ? mm : ty * (a.isy / p.hsy) * p.hw + tx * (a.isx / p.hsx);
   }
   // per-chunk opaque copy of hbase: the per-tap fragment addresses are then computed in the chunk,
   // not hoisted out of the chunk loop as NTAPS x TM live registers (which spilled)
@@ -225,8 +246,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
     split_quad(i, 0, smem);
     load_quad(i, 1 < nchunks ? 1 : 0);
   }
-  load_b(0, fb[0]);
-  load_b(1, fb[1]);
+#pragma unroll
+  for (int q = 0; q < PD; ++q) load_b(q, fb[q]);
   __syncthreads();
 
   // one chunk; KS = chunk index mod KU (compile-time), so step s = k*NTAPS + t sits in ring slot
@@ -261,7 +282,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
       // kept in this order by the scheduling barriers: the prefetches are issued before this
       // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
 #if !(WD_ABL & 2)
-      load_b(k * NTAPS + t + 2, fb[(sr + 2) % R]);
+      load_b(k * NTAPS + t + PD, fb[(sr + PD) % R]);
 #endif
       if (t + 1 < NTAPS) {
         toff += p.xstep;
@@ -300,38 +321,41 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const li
 
   // with WD_ALT an even chunk count leaves the running sum negated
   const float oscale = (WD_ALT && nchunks > 0 && !(nchunks & 1)) ? -SM::scale : SM::scale;
-  // every accumulator tile of the wave is staged in LDS first (the plane sets are free after the
-  // last barrier): the accumulators are dead before the epilogue loads its operands
   constexpr int CTS = 32 * 33;
-  float* ct = (float*)smem + wave * (TM * TN * CTS);
+  if constexpr (EPI_ALL) {
+    // every accumulator tile of the wave is staged in LDS first (the plane sets are free after the
+    // last barrier): the accumulators are dead before the epilogue loads its operands
+    float* ct = (float*)smem + wave * (TM * TN * CTS);
 #pragma unroll
-  for (int qq = 0; qq < TM * TN; ++qq)
+    for (int qq = 0; qq < TM * TN; ++qq)
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      ct[qq * CTS + ((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * oscale;
-  auto stage = [&](int) {};
+      for (int r = 0; r < 16; ++r)
+        ct[qq * CTS + ((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * oscale;
+    auto stage = [&](int) {};
 #if WD_ABL & 8
-  {
-    float z = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) z += acc[i][j][r];
-    if (z == 1234.5f) ((float*)a.y)[tid] = z;
-    return;
-  }
+    if (ct[0] != 1234.5f) return;
 #endif
-  epilogue_all<float, TM * TN, TN, decltype(stage), CTS>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN,
-                                                          lane, stage);
+    epilogue_all<float, TM * TN, TN, decltype(stage), CTS>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN,
+                                                            lane, stage);
+  } else {
+    float* ct = (float*)smem + wave * CTS;
+    epilogue_all<float, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, [&](int q) {
+#pragma unroll
+      for (int qq = 0; qq < TM * TN; ++qq)
+        if (qq == q) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            ct[((r & 3) + 8 * (r >> 2) + 4 * lhalf) * 33 + lrow] = acc[qq / TN][qq % TN][r] * oscale;
+        }
+    });
+  }
 }
 
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ>
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0>
 static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   constexpr int NT = WM * WN * 64;
   constexpr int NPA = SplitMode<MODE>::NPA;
-  if (a.ntaps != NTAPS || a.copad % 32 || a.cpad % 16 || a.ci % 4 || a.ldx % 4 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt_split % 16))
+  if (a.ntaps != (VT > 0 ? 1 : NTAPS) || a.copad % 32 || a.cpad % (16 * (VT > 0 ? VT : 1)) || a.ci % 4 || a.ldx % 4 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt_split % 16))
     return 0;
   if ((int64_t)a.n * a.h * a.w * a.ldx >= (1LL << 31)) return 0;
   WdPlan p;
@@ -356,7 +380,7 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   p.hh = ((TH - 1) * a.isy + (dymax - dymin)) / p.hsy + 1;
   p.hw = ((TW - 1) * a.isx + (dxmax - dxmin)) / p.hsx + 1;
   p.hpix = p.hh * p.hw;
-  if ((p.hpix + NT / 4 - 1) / (NT / 4) > NQ) return 0;     // the halo needs more quads per thread
+  if (((VT > 0 ? VT * TH * TW : p.hpix) + NT / 4 - 1) / (NT / 4) > NQ) return 0;   // more quads than NQ
   if ((int64_t)a.n * a.h * a.w * a.ldx * 4 >= (1LL << 31)) return 0;   // buffer-load byte offsets
   p.plane_bytes = NQ * (NT / 4) * 32;   // every quad's pixel, valid or not (unconditional stores)
   p.set_bytes = NPA * p.plane_bytes;
@@ -371,12 +395,19 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   p.nx = nx;
   p.ystep = (sy / p.hsy) * p.hw;
   p.xstep = sx / p.hsx;
+  if (VT > 0) {   // 1x1: VT blocks of the tile's BM pixels, virtual tap t = block t
+    p.hpix = VT * TH * TW;
+    p.toff0 = 0;
+    p.nx = VT;
+    p.xstep = TH * TW;
+    p.ystep = 0;
+  }
   p.tiles_y = (a.mi + TH - 1) / TH;
   p.tiles_x = (a.mj + TW - 1) / TW;
-  p.nchunks = a.cpad / 16;
+  p.nchunks = a.cpad / (16 * (VT > 0 ? VT : 1));
   const int tail = TH * TW * 4 + BN * 4;
   constexpr int TQ = (TH * TW / WM / 32) * (BN / WN / 32);   // accumulator tiles per wave
-  const int epi_bytes = (NT / 64) * TQ * 32 * 33 * 4;
+  const int epi_bytes = (NT / 64) * (TQ <= 4 ? TQ : 1) * 32 * 33 * 4;
   // LDS plan: two plane sets when two workgroups still fit a CU, else one set at two per CU,
   // else the single-workgroup plans
   auto need = [&](int sets) { return (sets * p.set_bytes > epi_bytes ? sets * p.set_bytes : epi_bytes) + tail; };
@@ -388,7 +419,7 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   if ((int64_t)(a.copad / 32) * p.nchunks * NTAPS * SplitMode<MODE>::NPB * 1024 >= (1LL << 31)) return 0;
   dim3 grid((unsigned)blocks, (a.copad + BN - 1) / BN);
-  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ>;
+  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
     status = fail(std::string("split wd conv: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -409,6 +440,10 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   auto blocks = [&](int th, int tw, int bn) {
     return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
   };
+  // 1x1 (qkv / proj Linear, GDN x^2, skips): 8x16 px x 192 channels, two 16-channel chunks per
+  // barrier -- the split of an activation is shared by all 192 output channels
+  if (a.ntaps == 1 && a.mi >= 8 && a.mj >= 16 && (int64_t)a.n * a.mi * a.mj >= 65536 && a.cpad % 32 == 0)
+    return try_split_wd<2, 2, 8, 16, 192, 2, 2, 4, 2>(a, s, status);
   if (a.mi > 8 && a.mj > 8 && blocks(16, 16, 64) >= 256) {
     switch (a.ntaps) {
       case 9: return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3, ConvT phase 3x3

@@ -31,6 +31,8 @@ DEV = "cuda"
     (192, 192, 1, 1, (0, 0, 0, 0), 8, 128, "square"),  # GDN: conv1x1(x^2) (prologue SQUARE)
     (96, 96, 1, 1, (0, 0, 0, 0), 8, 50, "gate"),       # 1x1 GEMM: ragged M, copad 96 (clamped n-tiles)
     (192, 192, 1, 1, (0, 0, 0, 0), 8, 64, "gdn"),      # 1x1 GEMM: x^2 prologue + GDN x*rsqrt(n) epilogue
+    (192, 192, 1, 1, (0, 0, 0, 0), 16, 64, "gdn"),     # 1x1 on the weights-direct kernel's virtual taps
+    (96, 96, 1, 1, (0, 0, 0, 0), 32, 60, "gate"),      # virtual taps: ragged tiles, copad 96 < BN 192
 ])
 def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     if mode == 1 and (cout % 64 or epi == "gdn"):
