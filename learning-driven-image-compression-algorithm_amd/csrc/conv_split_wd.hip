@@ -52,8 +52,10 @@ struct WdPlan {
 
 // VT > 0: a 1x1 convolution whose NTAPS = VT "virtual taps" are VT consecutive 16-channel chunks
 // staged together (one barrier per VT chunks; the halo is the tile itself, VT blocks of BM pixels).
+// Occupancy: two waves per SIMD, four for the one-tile-per-wave small-map configurations (TM = TN = 1).
 template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0>
-__global__ __launch_bounds__(WM * WN * 64, 2) void conv_split_wd_kernel(const lic_conv_args a, const WdPlan p) {
+__global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32) ? 4 : 2) void conv_split_wd_kernel(
+    const lic_conv_args a, const WdPlan p) {
   using SM = SplitMode<MODE>;
   using T = typename SM::T;
   constexpr int NPA = SM::NPA, NPB = SM::NPB, NPROD = SM::NPROD;
@@ -444,6 +446,12 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   // barrier -- the split of an activation is shared by all 192 output channels
   if (a.ntaps == 1 && a.mi >= 8 && a.mj >= 16 && (int64_t)a.n * a.mi * a.mj >= 65536 && a.cpad % 32 == 0)
     return try_split_wd<2, 2, 8, 16, 192, 2, 2, 4, 2>(a, s, status);
+  // the 16x16 latents of the slice loop / hyper nets (B x 256 px): 8x8 px x 64 channel tiles, one
+  // 32x32 accumulator per wave, four waves per SIMD -- the grid is what limits these launches
+  if (a.mi >= 8 && a.mj >= 8 && blocks(16, 16, 64) < 256 && blocks(8, 8, 64) >= 64) {
+    if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
+    if (a.ntaps == 9) return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);
+  }
   if (a.mi > 8 && a.mj > 8 && blocks(16, 16, 64) >= 256) {
     switch (a.ntaps) {
       case 9: return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3, ConvT phase 3x3

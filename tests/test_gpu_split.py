@@ -33,6 +33,8 @@ DEV = "cuda"
     (192, 192, 1, 1, (0, 0, 0, 0), 8, 64, "gdn"),      # 1x1 GEMM: x^2 prologue + GDN x*rsqrt(n) epilogue
     (192, 192, 1, 1, (0, 0, 0, 0), 16, 64, "gdn"),     # 1x1 on the weights-direct kernel's virtual taps
     (96, 96, 1, 1, (0, 0, 0, 0), 32, 60, "gate"),      # virtual taps: ragged tiles, copad 96 < BN 192
+    (128, 64, 1, 1, (0, 0, 0, 0), 32, 16, "gelu"),     # slice-loop 1x1 at 16^2: 8x8-px virtual-tap tiles
+    (224, 128, 3, 1, (1, 1, 1, 1), 32, 16, "plain"),   # slice-loop cc transform (8x8 px x 64 ch tiles)
 ])
 def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     if mode == 1 and (cout % 64 or epi == "gdn"):
