@@ -13,7 +13,8 @@ The headline runs at fp32 grade (the reference computes in fp32, model/net_ga.py
 conv product formed from six bf16 MFMA products of exact three-part splits (all 24 significand
 bits, fp32 exponent range, dropped terms <= 2^-26 relative; csrc/conv_halo_split.hip) -- when
 its parity leg on the TIMED batch (seed-0 weights, seed-1000 input of rank 0) meets the
-north-star bar with 0 flipped symbols, else exact fp32 (v_mfma_f32_32x32x2_f32).  Extra
+north-star bar with no more flipped symbols (oracle near-ties and their cascades) than the
+exact-fp32 path on the same batch, else exact fp32 (v_mfma_f32_32x32x2_f32).  Extra
 fields: roofline (dominant kernel: the 3x3 192->192 convolution of Win_noShift_Attention at
 64x64, timed with HIP events on its launch stream, against the matching MFMA peak),
 a_model (analysis stack, BASELINE config 2), cpu_baseline (the oracle restatement on this
@@ -51,7 +52,9 @@ def _env_int(k, d):
 PMC_FILES = {torch.float16: "profiles/r02/pmc_conv3x3_64_f16.json",
              torch.float32: "profiles/r02/pmc_conv3x3_64_f32.json",
              ("split", 1): "profiles/r02/pmc_conv3x3_64_f32x3.json",
-             ("split", 2): "profiles/r02/pmc_conv3x3_64_f32x6.json"}
+             ("split", 2): "profiles/r03/pmc_conv3x3_64_f32x6.json"}
+# the kernel that runs the roofline conv per precision (csrc/)
+ROOF_KERNEL = {0: "conv_halo_kernel", 1: "conv_halo_split_kernel", 2: "conv_split_wd_kernel"}
 # Net precision -> lic_conv_args.mfma_mode (lic_amd.functional.SPLIT_MODES)
 SPLIT_MODES = {"fp32x3": 1, "fp32x6": 2}
 # per split mode: 16-bit MFMA products per fp32 product, label
@@ -201,7 +204,8 @@ def parity_check(arch, precision, size, device, batch=1):
     """The timed batch (rank 0's input, the timed net's seed-0 weights) through the HIP path and
     the CPU oracle: bpp / PSNR deltas, the symbol flips and how many of them are near-ties of the
     oracle's y - mu (|frac - 1/2| < TIE_EPS: fp32 summation order, tests/parity.py), and whether
-    the north-star bar holds (bpp 1e-5, PSNR 1e-4 dB, flips at most 3e-5 of the symbols)."""
+    the north-star bar holds (bpp 1e-5, PSNR 1e-4 dB, flips at most 3e-5 of the symbols, each a
+    near-tie or its cascade)."""
     from oracle import ref_cpu as R
     net = build_net(arch, precision, size, batch, "cpu", seed=0)
     P = {k: v.detach().float() for k, v in net.state_dict().items()}
@@ -215,15 +219,25 @@ def parity_check(arch, precision, size, device, batch=1):
     ne = net.last["symbols"].cpu() != ref["symbols"]
     flips = int(ne.sum())
     d = ref["z3"] - ref["means"]
-    ties = int((ne & (((d - torch.floor(d)) - 0.5).abs() < TIE_EPS)).sum())
+    tie_mask = ne & (((d - torch.floor(d)) - 0.5).abs() < TIE_EPS)
+    ties = int(tie_mask.sum())
+    # every other flip must be a cascade: same image, a later slice, within the 8-pixel latent
+    # neighbourhood of a near-tie flip (a flipped y_hat of slice i moves mu of the later slices)
+    per_slice = ref["symbols"].shape[1] // 4
+    tl = tie_mask.nonzero().tolist()
+    unexplained = sum(1 for b, c, y, x in (ne & ~tie_mask).nonzero().tolist()
+                      if not any(tb == b and tc // per_slice < c // per_slice and abs(ty - y) < 8 and abs(tx - x) < 8
+                                 for tb, tc, ty, tx in tl))
     d_bpp = abs(bpp.item() - ref["bpp"].item())
     d_psnr = abs(v_psnr.item() - ref["v_psnr"].item())
     bar = 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (batch * size * size)
     return {"images": batch, "bpp": round(bpp.item(), 7), "bpp_ref": round(ref["bpp"].item(), 7),
             "d_bpp": d_bpp, "psnr_db": round(v_psnr.item(), 5), "d_psnr_db": d_psnr,
-            "symbol_flips": flips, "near_tie_flips": ties, "symbol_mismatch_frac": flips / ref["symbols"].numel(),
+            "symbol_flips": flips, "near_tie_flips": ties, "unexplained_flips": unexplained,
+            "symbol_mismatch_frac": flips / ref["symbols"].numel(),
             "batch": f"timed batch of rank 0 (weights seed 0, input seed 1000, {batch} x {size}x{size})",
-            "meets_north_star_bar": bool(d_bpp <= bar and d_psnr <= 1e-4 and flips / ne.numel() <= 3e-5)}
+            "meets_north_star_bar": bool(d_bpp <= bar and d_psnr <= 1e-4 and flips / ne.numel() <= 3e-5 and
+                                         unexplained == 0)}
 
 
 def forward_rate(net, x, iters=10):
@@ -285,8 +299,9 @@ def main():
     ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp32", "fp32x6", "fp32x3"],
                     help="auto (default): fp32x6 -- fp32 activations and accumulation, products from six bf16 "
                          "products of exact three-part splits (fp32 grade) -- when its parity leg on the timed "
-                         "batch meets the north-star bar with 0 flipped symbols (checked first, on rank 0), else "
-                         "exact fp32; fp32x3 (fp16 parts, narrower than fp32) and fp16 activations are extras")
+                         "batch meets the north-star bar with no more flipped symbols than exact fp32 on that batch "
+                         "(checked first, on rank 0), else exact fp32; fp32x3 (fp16 parts, narrower than fp32) and "
+                         "fp16 activations are extras")
     ap.add_argument("--no-extras", action="store_true", help="skip cpu baseline / parity / fp16 legs")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--post-processing", action="store_true", help="HAN post-processing head (eval_net flag)")
@@ -298,12 +313,14 @@ def main():
     rank, world, local = D.init("nccl")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    gate = None
+    gate = gate32 = None
     if args.precision == "auto":
         ok = 0.0
         if rank == 0:
             gate = parity_check(args.arch, "fp32x6", args.size, device, args.batch)
-            ok = 1.0 if gate["meets_north_star_bar"] and gate["symbol_flips"] == 0 else 0.0
+            gate32 = parity_check(args.arch, "fp32", args.size, device, args.batch)
+            ok = 1.0 if (gate["meets_north_star_bar"] and
+                         gate["symbol_flips"] <= gate32["symbol_flips"]) else 0.0
         ok = D.max_over_ranks(ok, world, device)
         args.precision = "fp32x6" if ok > 0 else "fp32"
         torch.cuda.empty_cache()
@@ -368,10 +385,10 @@ def main():
                        "parallelism": f"image-sharded x{world} (independent batches, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": _pmc_traffic(("split", split) if split else dtype, args.batch, args.size),
-                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} (conv_halo_kernel {dname}), "
+                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} ({ROOF_KERNEL[split]} {dname}), "
                                    f"{flops / 1e9:.1f} GFLOP/launch, {tk * 1e6:.1f} us/launch",
                          "peak_note": (f"16-bit dense MFMA / {SPLIT_PRODUCTS[split]} (each fp32 product = "
-                                       f"{SPLIT_PRODUCTS[split]} 16-bit MFMA products, csrc/conv_halo_split.hip)"
+                                       f"{SPLIT_PRODUCTS[split]} 16-bit MFMA products, csrc/conv_split.h)"
                                        if split else
                                        "fp32-input MFMA v_mfma_f32_32x32x2_f32 (exact fp32, 1/16 of the fp16 rate)"
                                        if dtype == torch.float32 else "fp16 dense MFMA"),
@@ -389,15 +406,19 @@ def main():
                                       "cpu_baseline": cpu_baseline(args.arch, args.size, n_img=16, reps=5,
                                                                    what="a_model")}
             result["parity"] = (gate if gate is not None and args.precision == "fp32x6" else
+                                gate32 if gate32 is not None and args.precision == "fp32" else
                                 parity_check(args.arch, args.precision, args.size, device, args.batch))
             for other in [p for p in ("fp32", "fp32x6", "fp32x3", "fp16") if p != args.precision]:
                 result[other] = extra_leg(args, other, x, device, gf_a)
         if gate is not None:
             result["precision_gate"] = {
                 "rule": "headline = fp32x6 (fp32 grade) when its parity leg on the timed batch (rank 0's input, "
-                        "the timed seed-0 weights, CPU oracle) meets bpp 1e-5 / PSNR 1e-4 dB with 0 symbol flips, "
-                        "else exact fp32",
-                "fp32x6_parity": gate, "chosen": args.precision}
+                        "the timed seed-0 weights, CPU oracle) meets the north-star bar (bpp 1e-5, PSNR 1e-4 dB, "
+                        "every symbol flip an oracle near-tie |frac(y-mu)-1/2| < 2e-4 or its cascade) with no more "
+                        "flips than the exact-fp32 path on the same batch, else exact fp32.  0 flips is not "
+                        "attainable by any fp32 summation order other than the oracle's own on this batch: the "
+                        "exact-fp32 path flips its near-ties too (exact_fp32_parity)",
+                "fp32x6_parity": gate, "exact_fp32_parity": gate32, "chosen": args.precision}
         print(json.dumps(result), flush=True)
     D.finish(world)
 

@@ -387,6 +387,9 @@ static int split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
 // 0 to let the caller run the exact-fp32 kernels.
 int conv_halo_split_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   if ((a.mfma_mode != 1 && a.mfma_mode != 2) || !a.wgt_split || a.dtype != LIC_F32) return 0;
+  // one 16-channel chunk (the image-side 3x3 s2 of a 4-channel input): the exact-fp32 kernels are
+  // faster than a split pass whose cost is not amortised over any channel reduction
+  if (a.cpad <= 16) return 0;
   if (a.groups != 1 || a.ntaps < 1 || a.force_direct || a.force_mfma_generic) return 0;
   if (a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE && a.prologue != LIC_PRO_ABS) return 0;
   return a.mfma_mode == 1 ? split_dispatch<1>(a, s, status) : split_dispatch<2>(a, s, status);

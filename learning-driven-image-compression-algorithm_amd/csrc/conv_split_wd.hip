@@ -31,6 +31,11 @@
 #ifndef WD_SB
 #define WD_SB 0
 #endif
+// cache policy of the halo loads (2 = nt: the activations are streamed once, the weight fragments
+// that every workgroup re-reads should stay in L2)
+#ifndef WD_HALO_AUX
+#define WD_HALO_AUX 0
+#endif
 #ifndef WD_ALT
 #define WD_ALT 1
 #endif
@@ -76,6 +81,9 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   static_assert(VT == 0 || VT == NTAPS, "virtual taps");
   // every accumulator tile staged before the epilogue when that fits the plane sets (TM*TN <= 4)
   constexpr bool EPI_ALL = TM * TN <= 4;
+  // LDS plane geometry is compile-time (every quad's pixel has a slot): the part offsets fold into
+  // the ds_read / ds_write immediate offsets
+  constexpr int PLANE = NQ * (NT / 4) * 32, SET = NPA * PLANE;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* rowpix = (int*)(smem + p.rp_off);
@@ -148,7 +156,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
     int cq;
     const int q = quad_off(i, cq);
     const unsigned off = (q >= 0 && k * CSTEP + cq < a.ci) ? (unsigned)(q + k * CSTEP) * 4u : 0x80000000u;
-    hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
+    hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, WD_HALO_AUX);
   };
   // every quad stores (plane_bytes covers NQ * NT/4 pixels): no per-lane branch around the stores
   auto split_quad = [&](int i, int k, char* set) {
@@ -160,7 +168,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
                  pro, sg, parts);
     const int off = hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
 #pragma unroll
-    for (int pl = 0; pl < NPA; ++pl) *(uint2*)(set + pl * p.plane_bytes + off) = parts[pl];
+    for (int pl = 0; pl < NPA; ++pl) *(uint2*)(set + pl * PLANE + off) = parts[pl];
   };
 
   int hbase[TM];
@@ -179,7 +187,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
     for (int i = 0; i < TM; ++i) {
       const int hp = hb[i] + toff;
       const int o = hp * 32 + ((lhalf ^ ((hp >> 3) & 1)) << 4);
-      fa[pl][i] = *(const u32x4*)(set + pl * p.plane_bytes + o);
+      fa[pl][i] = *(const u32x4*)(set + pl * PLANE + o);
     }
   };
   // B fragments of step s = chunk * NTAPS + tap (clamped): n-tile (n0/32 + wn*TN + j), 1 KB per part,
@@ -260,8 +268,8 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   constexpr int QPS = (NQ + NTAPS - 1) / NTAPS;
   auto chunk = [&](int k, auto ks) {
     constexpr int KS = decltype(ks)::value;
-    const char* set = smem + (k & 1) * p.set_bytes;
-    char* nset = smem + ((k + 1) & 1) * p.set_bytes;
+    const char* set = smem + (k & 1) * SET;
+    char* nset = smem + ((k + 1) & 1) * SET;
     const int kn = k + 2 < nchunks ? k + 2 : nchunks - 1;
 #if WD_ALT
     if (k > 0)   // exact sign flip: the running sum changes sign with the chunk's parts
@@ -456,7 +464,8 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     switch (a.ntaps) {
       case 9: return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3, ConvT phase 3x3
       case 6: return try_split_wd<2, 6, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phases 3x2 / 2x3
-      case 4: return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phase 2x2
+      case 4: return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phase 2x2, 3x3 s2 phase
+      case 2: return try_split_wd<2, 2, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3 s2 phases 2x1 / 1x2
       case 49: return try_split_wd<2, 49, 16, 16, 64, 4, 2, 4>(a, s, status);   // 7x7: 8 waves, 22x22 halo
       default: break;
     }

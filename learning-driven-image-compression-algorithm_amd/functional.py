@@ -350,12 +350,12 @@ def split_weights(pk: ConvPack, mode: int = 1) -> Optional[torch.Tensor]:
 
 
 def stride2_phase_packs(pk: ConvPack) -> Optional[List[ConvPack]]:
-    """The input-parity phases of a stride-2 k x k ConvPack (k >= 4): four sub-packs holding the taps
-    whose row / column offsets share one parity (5x5: 9, 6, 6 and 4 taps), biased only in the
-    first.  Each phase reads every other input row and column, so the split kernel stages a
+    """The input-parity phases of a stride-2 k x k ConvPack (k >= 3, more than 16 input channels):
+    four sub-packs holding the taps whose row / column offsets share one parity (5x5: 9, 6, 6 and
+    4 taps; 3x3: 4, 2, 2, 1), biased only in the first.  Each phase reads every other input row and column, so the split kernel stages a
     quarter of the stride-2 halo (conv_split_wd.hip, hsy / hsx); the four launches accumulate into
     one output (csrc/conv.hip).  Cached on the pack."""
-    if pk.stride != 2 or pk.phase is not None or pk.groups != 1 or min(pk.kh, pk.kw) < 4 or \
+    if pk.stride != 2 or pk.phase is not None or pk.groups != 1 or min(pk.kh, pk.kw) < 3 or pk.cpad <= 16 or \
             pk.__dict__.get("_s2phase_of") is not None:
         return None
     sub = pk.__dict__.get("_s2phases")

@@ -38,6 +38,26 @@ def check_symbols(sym_gpu: torch.Tensor, ref: dict, max_rate: float = 3e-5) -> i
     return n
 
 
+def check_flip_sets_match(flipped_a: torch.Tensor, flipped_b: torch.Tensor, ref: dict, tie: float = 1e-6) -> int:
+    """Two fp32-grade paths (e.g. exact-fp32 MFMA and fp32x6) flip the same symbols against the
+    oracle, except (a) symbols whose oracle y - mu is within `tie` of the .5 boundary (a few fp32
+    ulps: any two summation orders may round such a tie either way) and (b) their cascades -- a
+    symbol of a later slice within the same 8-pixel latent neighbourhood of such a tie difference
+    (a flipped y_hat of slice i moves mu of the later slices, net_ga.py:1021-1067).  Returns the
+    size of the symmetric difference."""
+    d = ref["z3"] - ref["means"]
+    dist = ((d - torch.floor(d)) - 0.5).abs()
+    diff = flipped_a ^ flipped_b
+    ties = (diff & (dist < tie)).nonzero().tolist()
+    per_slice = ref["symbols"].shape[1] // 4
+    for b, c, y, x in (diff & (dist >= tie)).nonzero().tolist():
+        ok = any(tb == b and tc // per_slice < c // per_slice and abs(ty - y) < 8 and abs(tx - x) < 8
+                 for tb, tc, ty, tx in ties)
+        assert ok, f"flip-set difference at {(b, c, y, x)} is neither an oracle tie nor its cascade " \
+                   f"(|frac-0.5| = {dist[b, c, y, x]:.3e})"
+    return int(diff.sum())
+
+
 def _u8(x_rec):
     return torch.round(torch.clamp((x_rec.float().cpu() + 1) * 127.5, 0, 255)).to(torch.int32)
 

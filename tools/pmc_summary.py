@@ -36,7 +36,7 @@ def main():
            "WRITE_SIZE_kb_per_dispatch_median": wkb, "dispatches": [len(fe), len(wr)],
            "correction": "gfx950: FETCH_SIZE counts half the bytes of 16 B/lane streaming reads -> x2; WRITE_SIZE exact",
            "hbm_read_bytes": rd, "hbm_write_bytes": wb, "traffic_bytes_per_launch": rd + wb,
-           "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": round((rd + wb) / alg, 3), "round": "r02"}
+           "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": round((rd + wb) / alg, 3), "round": os.environ.get("LIC_ROUND", "r03")}
     with open(out, "w") as f:
         json.dump(rep, f, indent=1)
     print(json.dumps(rep))
