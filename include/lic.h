@@ -132,6 +132,8 @@ typedef struct lic_attn_args {
   int32_t scale_after; /* 0: q*scale before dot, 1: dot*scale */
   float scale;         /* head_dim ** -0.5 (as the reference's Python float, cast to fp32) */
   int32_t force_valu;  /* 1: skip the MFMA kernel (ws 8, head_dim <= 32) - testing only */
+  int32_t mfma_mode;   /* fp32 data: 0 exact fp32 MFMA; 2 "fp32x6": Q, K, V, P split into three bf16
+                          parts, 6 part products per dot (as lic_conv_args.mfma_mode 2) (abi 4) */
 } lic_attn_args;
 int lic_win_attn_fwd(const lic_attn_args* a, lic_stream_t stream);
 
@@ -480,7 +482,7 @@ int lic_dwconv_wgrad(int32_t dtype, const void* x, int32_t ldx, const void* dz, 
  * changes (3: lic_conv_args.mfma_mode / wgt_split, lic_rate_train_* seed_dev / seed_mul).  A
  * caller compiled against this header checks lic_abi_version() == LIC_ABI_VERSION and
  * lic_args_size(k) == sizeof(...) once after loading the library (the Python host does, _ffi.load). */
-#define LIC_ABI_VERSION 3
+#define LIC_ABI_VERSION 4
 enum { LIC_ARGS_CONV = 0, LIC_ARGS_ATTN = 1, LIC_ARGS_RATE = 2, LIC_ARGS_RANS = 3, LIC_ARGS_WGRAD = 4 };
 const char* lic_last_error(void);
 const char* lic_version(void);

@@ -18,7 +18,7 @@ ACT_NONE, ACT_RELU, ACT_LRELU, ACT_GELU, ACT_ROUND = 0, 1, 2, 3, 4
 PRO_NONE, PRO_SQUARE, PRO_ABS = 0, 1, 2
 EPI_PLAIN, EPI_GATE, EPI_HALF_TANH, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, EPI_RES_ACT = 0, 1, 2, 3, 4, 5, 6
 MAX_TAPS = 64
-ABI_VERSION = 3   # include/lic.h LIC_ABI_VERSION
+ABI_VERSION = 4   # include/lic.h LIC_ABI_VERSION
 
 EXPORTED_SYMBOLS = (
     "lic_conv2d_fwd", "lic_gdn_prepare", "lic_win_attn_fwd", "lic_layernorm_fwd",
@@ -80,7 +80,7 @@ class AttnArgs(ctypes.Structure):
         ("heads", _i32), ("ws", _i32), ("shift", _i32),
         ("table", _vp), ("tab_sr", _i32), ("tab_sh", _i32),
         ("mask_kind", _i32), ("scale_after", _i32), ("scale", _f32),
-        ("force_valu", _i32),
+        ("force_valu", _i32), ("mfma_mode", _i32),
     ]
 
 

@@ -182,6 +182,8 @@ extern "C" int lic_win_attn_fwd(const lic_attn_args* a, lic_stream_t stream) {
   if (a->heads <= 0 || a->c % a->heads) return fail("attn: C % heads != 0");
   if (a->h % a->ws || a->w % a->ws) return fail("attn: H, W must be multiples of the window");
   if (a->shift < 0 || a->shift >= a->ws) return fail("attn: 0 <= shift < ws");
+  if (a->mfma_mode != 0 && !(a->mfma_mode == 2 && a->dtype == LIC_F32))
+    return fail("attn: mfma_mode must be 0, or 2 with fp32 data");
   if (a->n * (int64_t)a->h * a->w == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == LIC_F32) return attn_dispatch<float>(*a, s);

@@ -11,17 +11,33 @@
 // stored as 8/16-byte runs at the query's original (un-rolled) pixel.
 //   fp16: v_mfma_f32_32x32x16_f16 (head_dim padded to 16/32 with zeros)
 //   fp32: v_mfma_f32_32x32x2_f32 (exact fp32 products)
+//   fp32, mfma_mode 2 ("fp32x6", SPLIT): Q, K, V and P split on the fly into three bf16 parts
+//         (conv_split.h), each dot as the 6 part products x0y0 + x0y1 + x1y0 + x0y2 + x1y1 + x2y0
+//         on v_mfma_f32_32x32x16_bf16 in the fp16 path's fragment layout (96 MFMAs of 32 cycles
+//         per wave instead of 128 of 64 cycles; dropped terms <= 2^-26 of each product)
 // Score = dot*scale + rel-pos bias (+ -100 region mask for WBA, -inf last
 // row/column mask for WMSA), softmax as max / exp(s-max) / sum / divide.
 #include "lic_common.h"
+#include "conv_split.h"
 
 namespace lic {
 
 constexpr int AT_N = 64;   // tokens per window (ws = 8)
 constexpr int VT_LD = 68;  // padded row (elements) of the V^T staging image
 
-template <typename T, int NW>
+// 8 fp32 values (two float4) -> their three bf16 parts as MFMA fragments (8 x 16-bit each)
+__device__ __forceinline__ void split8_bf16(float4 lo, float4 hi, u32x4 (&out)[3]) {
+  uint2 pl[3], ph[3];
+  split4<2>(lo, LIC_PRO_NONE, 1.f, pl);
+  split4<2>(hi, LIC_PRO_NONE, 1.f, ph);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) out[p] = u32x4{pl[p].x, pl[p].y, ph[p].x, ph[p].y};
+}
+
+template <typename T, int NW, int SPLIT = 0>
 __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_args a) {
+  static_assert(!SPLIT || sizeof(T) == 4, "split products are for fp32 data");
+  using SM = SplitMode<2>;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lr = lane & 31, lh = lane >> 5;
   const int d = a.c / a.heads;
@@ -111,6 +127,36 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
           S[tj][ti] = mfma_k16<T>(kf[s][tj], qf[s][ti], S[tj][ti]);
+    }
+  } else if constexpr (SPLIT) {
+    // lane (row, h) splits channels 16s + 8h .. +7 of its key / (pre-scaled) query rows
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (16 * s >= d) break;
+      const int ch = 16 * s + 8 * lh;
+      u32x4 kp[2][3], qp[2][3];
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const float* tp = (const float*)qkv + (int64_t)(t2 ? pix_lr1 : pix_lr0) * ldq;
+        float4 k0 = make_float4(0.f, 0.f, 0.f, 0.f), k1 = k0, q0 = k0, q1 = k0;
+        if (ch < d) {
+          k0 = *(const float4*)(tp + koff + ch);
+          k1 = *(const float4*)(tp + koff + ch + 4);
+          q0 = *(const float4*)(tp + qoff + ch);
+          q1 = *(const float4*)(tp + qoff + ch + 4);
+        }
+        q0 = make_float4(q0.x * pre, q0.y * pre, q0.z * pre, q0.w * pre);
+        q1 = make_float4(q1.x * pre, q1.y * pre, q1.z * pre, q1.w * pre);
+        split8_bf16(k0, k1, kp[t2]);
+        split8_bf16(q0, q1, qp[t2]);
+      }
+#pragma unroll
+      for (int pr = SM::NPROD - 1; pr >= 0; --pr)   // smallest products first
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < 2; ++ti)
+            S[tj][ti] = mfma_k16<bf16_t>(kp[tj][SM::PA[pr]], qp[ti][SM::PB[pr]], S[tj][ti]);
     }
   } else {
     for (int k = 0; k < d; k += 2) {
@@ -219,6 +265,25 @@ __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_a
           O[ti] = mfma_k16<T>(va, pb, O[ti]);
         }
       }
+  } else if constexpr (SPLIT) {
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int j0 = 32 * tj + 16 * s2 + 4 * lh;
+        u32x4 vp[3];
+        split8_bf16(*(const float4*)(vrow + j0), *(const float4*)(vrow + j0 + 8), vp);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti) {
+          const int r0 = 8 * s2;
+          u32x4 pp[3];
+          split8_bf16(make_float4(S[tj][ti][r0], S[tj][ti][r0 + 1], S[tj][ti][r0 + 2], S[tj][ti][r0 + 3]),
+                      make_float4(S[tj][ti][r0 + 4], S[tj][ti][r0 + 5], S[tj][ti][r0 + 6], S[tj][ti][r0 + 7]), pp);
+#pragma unroll
+          for (int pr = SM::NPROD - 1; pr >= 0; --pr)
+            O[ti] = mfma_k16<bf16_t>(vp[SM::PA[pr]], pp[SM::PB[pr]], O[ti]);
+        }
+      }
   } else {
 #pragma unroll
     for (int tj = 0; tj < 2; ++tj)
@@ -272,6 +337,8 @@ int win_attn_mfma_dispatch(const lic_attn_args& a, hipStream_t s, int& status) {
   } else if (a.dtype == LIC_BF16) {
     if (nw == 8) hipLaunchKernelGGL((win_attn_mfma_kernel<bf16_t, 8>), dim3((unsigned)blocks), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((win_attn_mfma_kernel<bf16_t, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  } else if (a.mfma_mode == 2) {
+    hipLaunchKernelGGL((win_attn_mfma_kernel<float, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL((win_attn_mfma_kernel<float, 4>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   }

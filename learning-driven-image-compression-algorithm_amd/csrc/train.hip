@@ -947,10 +947,17 @@ using namespace lic;
 
 static inline unsigned tr_nblk(int64_t total) { return (unsigned)((total + 255) / 256); }
 
+// wgrad_tr.hip: the tiled 16-bit kernel (all taps of a tap group per work-group, transpose reads)
+namespace lic {
+int wgrad_tr_nsplit(const lic_wgrad_args& a);
+int wgrad_tr_launch(const lic_wgrad_args& a, hipStream_t s, int* nsplit);
+}  // namespace lic
+
 extern "C" int64_t lic_conv2d_wgrad_workspace(const lic_wgrad_args* a) {
   if (!a || wgrad_check(*a)) return -1;
-  const WgPlan p = wgrad_plan(*a);
-  return (int64_t)p.nsplit * a->ntaps * a->co * a->ci * (int64_t)sizeof(float);
+  int ns = wgrad_tr_nsplit(*a);
+  if (!ns) ns = wgrad_plan(*a).nsplit;
+  return (int64_t)ns * a->ntaps * a->co * a->ci * (int64_t)sizeof(float);
 }
 
 extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {
@@ -958,11 +965,16 @@ extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {
   const lic_wgrad_args& a = *ap;
   if (int e = wgrad_check(a)) return e;
   const WgPlan p = wgrad_plan(a);
-  const int64_t need = (int64_t)p.nsplit * a.ntaps * a.co * a.ci * (int64_t)sizeof(float);
+  const int tr_ns = wgrad_tr_nsplit(a);
+  const int nsplit = tr_ns ? tr_ns : p.nsplit;
+  const int64_t need = (int64_t)nsplit * a.ntaps * a.co * a.ci * (int64_t)sizeof(float);
   if (!a.ws || a.ws_bytes < need)
     return fail("wgrad: workspace too small (" + std::to_string(a.ws_bytes) + " < " + std::to_string(need) + ")");
   hipStream_t s = (hipStream_t)stream;
-  if (a.dtype == LIC_F16) {
+  if (tr_ns) {
+    int ns = 0;
+    if (int e = wgrad_tr_launch(a, s, &ns)) return e;
+  } else if (a.dtype == LIC_F16) {
     if (p.bm == 128) wgrad_launch<half_t, 128, 128, 2, 2>(a, p, s);
     else wgrad_launch<half_t, 64, 64, 2, 2>(a, p, s);
   } else if (a.dtype == LIC_BF16) {
@@ -974,7 +986,7 @@ extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {
   }
   LIC_CHECK_LAUNCH();
   const int64_t total = (int64_t)a.ntaps * a.co_out * a.ci_out;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(tr_nblk(total)), dim3(256), 0, s, a.ws, p.nsplit, a.ntaps, a.co, a.ci,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(tr_nblk(total)), dim3(256), 0, s, a.ws, nsplit, a.ntaps, a.co, a.ci,
                      a.co_out, a.ci_out, a.dw, a.s_co, a.s_ci, a.s_tap, a.accumulate);
   LIC_CHECK_LAUNCH();
   return 0;

@@ -485,6 +485,7 @@ def win_attn(qkv: Act, C: int, heads: int, ws: int, shift: int, table: torch.Ten
     a.table, a.tab_sr, a.tab_sh = _dp(table), tab_sr, tab_sh
     a.mask_kind, a.scale_after, a.scale = mask_kind, 1 if scale_after else 0, scale
     a.force_valu = 1 if force_valu else 0
+    a.mfma_mode = 2 if (qkv.dtype == torch.float32 and split_mode() == 2) else 0
     check(_lib().lic_win_attn_fwd(ctypes.byref(a), stream_handle()))
     return out
 

@@ -83,6 +83,30 @@ def test_mfma_attention_matches_reference(dtype, C, heads, ws, shift, H, W, mask
         assert (out - valu).abs().max().item() <= tol * (ref.abs().max().item() + 1e-6)
 
 
+@pytest.mark.parametrize("C,heads,ws,shift,H,W,mask_kind,scale_after", CASES)
+def test_split_attention_fp32_grade(C, heads, ws, shift, H, W, mask_kind, scale_after):
+    """fp32 data under split mode 2 (fp32x6: Q, K, V, P as three bf16 parts, 6 part products)
+    against a float64 restatement: as close as the exact fp32 MFMA kernel (both errors at the
+    fp32 rounding level, 2e-6 of the output scale)."""
+    import lic_amd.functional as Fn
+    g = torch.Generator().manual_seed(C * 7 + H + W + shift)
+    qkv = torch.randn(2, H, W, 3 * C, generator=g)
+    table = torch.randn((2 * ws - 1) ** 2, heads, generator=g) * 0.5
+    scale = (C // heads) ** -0.5
+    ref = _attn_ref(qkv.double(), C, heads, ws, shift, table.double(), mask_kind, scale_after, scale).float()
+    exact = _run(qkv, C, heads, ws, shift, table, mask_kind, scale_after, scale, torch.float32, False)
+    prev = Fn.split_mode()
+    Fn.set_split_mode(2)
+    try:
+        split = _run(qkv, C, heads, ws, shift, table, mask_kind, scale_after, scale, torch.float32, False)
+    finally:
+        Fn.set_split_mode(prev)
+    amax = ref.abs().max().item()
+    e_split = (split - ref).abs().max().item()
+    e_exact = (exact - ref).abs().max().item()
+    assert e_split <= 2e-6 * amax, (e_split, e_exact, amax)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_mfma_attention_strided_views(dtype):
     """qkv and out as channel windows of wider NHWC buffers (ld > 3C, c0 > 0)."""
