@@ -456,6 +456,12 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     return try_split_wd<2, 2, 8, 16, 192, 2, 2, 4, 2>(a, s, status);
   // the 16x16 latents of the slice loop / hyper nets (B x 256 px): 8x8 px x 64 channel tiles, one
   // 32x32 accumulator per wave, four waves per SIMD -- the grid is what limits these launches
+  // 32 output channels (the slice loop's per-slice mean / scale heads): 8x8 px x 32 channel tiles of
+  // two waves, one 32x32 accumulator each
+  if (a.copad == 32 && a.mi >= 8 && a.mj >= 8) {
+    if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2>(a, s, status);
+    if (a.ntaps == 9) return try_split_wd<2, 9, 8, 8, 32, 2, 1, 4>(a, s, status);
+  }
   if (a.mi >= 8 && a.mj >= 8 && blocks(16, 16, 64) < 256 && blocks(8, 8, 64) >= 64) {
     if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
     if (a.ntaps == 9) return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);

@@ -7,7 +7,7 @@
 // x and dz exchanged, _ConvT2dFn.backward; GDN dGamma' with PRO_SQUARE).
 //
 // A work-group owns 64 output channels x 64 input channels x one tap group (all 9 taps of a
-// 3x3 window, one 5-tap row of a 5x5 window, or a single 1x1 tap) and walks a contiguous run
+// 3x3 window, one 5- or 7-tap row of a 5x5 / 7x7 window, or a single 1x1 tap) and walks a contiguous run
 // of spatial tiles (8 x 8 lattice pixels, 16 x 8 for 1x1) — the split-K dimension.  Per tile it
 // stages, with plain coalesced 16-byte loads (raw buffer loads: out-of-image rows and the ragged
 // lattice edge read as zeros):
@@ -36,7 +36,7 @@ struct WtrPlan {
 
 template <int S, int G> struct WtrCfg {
   static constexpr int SPY = G == 9 ? 2 : 0;               // tap-window spans the halo covers
-  static constexpr int SPX = G == 9 ? 2 : (G == 5 ? 4 : 0);
+  static constexpr int SPX = G == 9 ? 2 : (G == 1 ? 0 : G - 1);
   static constexpr int TI = G == 1 ? 16 : 8, TJ = 8;       // lattice tile (K per stage = TI*TJ)
   static constexpr int HR = (TI - 1) * S + SPY + 1, HC = (TJ - 1) * S + SPX + 1;
   static constexpr int HPIX = HR * HC, ZPIX = TI * TJ;
@@ -188,14 +188,14 @@ static bool wtr_enabled() {
   return on;
 }
 
-// Plans the tiled kernel; returns its tap-group size G (1, 5 or 9) or 0 when it does not apply
-// (fp32, strides other than 1 / 2, tap sets that are not 1x1, 3x3 or rows of 5, > 2 GB views).
+// Plans the tiled kernel; returns its tap-group size G (1, 5, 7 or 9) or 0 when it does not apply
+// (fp32, strides other than 1 / 2, tap sets that are not 1x1, 3x3 or rows of 5 / 7, > 2 GB views).
 static int wtr_plan(const lic_wgrad_args& a, WtrPlan& p) {
   if (!wtr_enabled() || a.dtype == LIC_F32) return 0;
   if (a.isy != a.isx || (a.isy != 1 && a.isy != 2)) return 0;
-  const int G = a.ntaps == 1 ? 1 : (a.ntaps == 9 ? 9 : (a.ntaps % 5 == 0 ? 5 : 0));
+  const int G = a.ntaps == 1 ? 1 : (a.ntaps == 9 ? 9 : (a.ntaps % 5 == 0 ? 5 : (a.ntaps % 7 == 0 ? 7 : 0)));
   if (!G) return 0;
-  const int spy = G == 9 ? 2 : 0, spx = G == 9 ? 2 : (G == 5 ? 4 : 0);
+  const int spy = G == 9 ? 2 : 0, spx = G == 9 ? 2 : (G == 1 ? 0 : G - 1);
   p.ngroups = a.ntaps / G;
   for (int g = 0; g < p.ngroups; ++g) {
     int ymin = 127, xmin = 127, ymax = -128, xmax = -128;
@@ -255,10 +255,12 @@ static int wtr_launch_t(const lic_wgrad_args& a, const WtrPlan& p, int G, hipStr
   if (a.isy == 1) {
     if (G == 9) return wtr_launch<T, 1, 9>(a, p, s);
     if (G == 5) return wtr_launch<T, 1, 5>(a, p, s);
+    if (G == 7) return wtr_launch<T, 1, 7>(a, p, s);
     return wtr_launch<T, 1, 1>(a, p, s);
   }
   if (G == 9) return wtr_launch<T, 2, 9>(a, p, s);
   if (G == 5) return wtr_launch<T, 2, 5>(a, p, s);
+  if (G == 7) return wtr_launch<T, 2, 7>(a, p, s);
   return wtr_launch<T, 2, 1>(a, p, s);
 }
 

@@ -1,5 +1,5 @@
-"""Weight gradient of the 16-bit training path (lic_conv2d_wgrad -> wgrad_tr_kernel for 1x1, 3x3
-and 5x5 tap windows, wgrad_kernel otherwise) against float64 torch on the SAME 16-bit operands.
+"""Weight gradient of the 16-bit training path (lic_conv2d_wgrad -> wgrad_tr_kernel for 1x1, 3x3,
+5x5 and 7x7 tap windows, wgrad_kernel otherwise) against float64 torch on the SAME 16-bit operands.
 
 Both sides see identical bf16 / fp16 inputs, so the only difference is the fp32 MFMA
 accumulation order: the bar is 2e-5 of the gradient's max magnitude (an indexing error — a
@@ -34,7 +34,9 @@ def _check(dw, ref, name):
     (2, 16, 16, 32, 64, 5, 2, (1, 1, 2, 2)),       # ZeroPad2d((1, 2, 1, 2)) + conv5x5 s2
     (2, 17, 15, 64, 64, 3, 2, (1, 1, 1, 1)),       # conv3x3 s2, odd map
     (1, 12, 12, 64, 32, 5, 1, (2, 2, 2, 2)),       # 5x5 s1 (rows of 5 taps)
-    (1, 12, 12, 32, 64, 7, 1, (3, 3, 3, 3)),       # 7x7: the generic kernel
+    (1, 12, 12, 32, 64, 7, 1, (3, 3, 3, 3)),       # 7x7 (rows of 7 taps)
+    (1, 10, 10, 32, 64, 7, 2, (3, 3, 3, 3)),       # 7x7 s2
+    (1, 11, 13, 32, 48, 2, 1, (0, 0, 1, 1)),       # 2x2: the generic kernel
     (1, 9, 9, 16, 64, 1, 2, (0, 0, 0, 0)),         # 1x1 s2
 ])
 def test_conv_wgrad(dtype, B, H, W, ci, co, k, s, pad):

@@ -36,6 +36,9 @@ SHAPES = [
     ("lin512_128@16", 512, 128, 1, 1, (0, 0, 0, 0), 16),
     ("proj1x1@64", 192, 192, 1, 1, (0, 0, 0, 0), 64),
     ("gdn1x1@128", 192, 192, 1, 1, (0, 0, 0, 0), 128),
+    ("cc3x3_128_32@16", 128, 32, 3, 1, (1, 1, 1, 1), 16),
+    ("cc3x3_224_32@16", 224, 32, 3, 1, (1, 1, 1, 1), 16),
+    ("cc1x1_128_32@16", 128, 32, 1, 1, (0, 0, 0, 0), 16),
 ]
 
 

@@ -27,6 +27,7 @@ SHAPES = [
     ("5x5_192@32", 192, 192, 5, 1, (2, 2, 2, 2), 32),
     ("1x1_192@64", 192, 192, 1, 1, (0, 0, 0, 0), 64),
     ("1x1_192@128", 192, 192, 1, 1, (0, 0, 0, 0), 128),
+    ("7x7_256@32", 256, 256, 7, 1, (3, 3, 3, 3), 32),
 ]
 
 
