@@ -28,19 +28,22 @@ typedef short v4s16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s16 lds_v4s16;
 
 struct WtrPlan {
-  int tiles_i, tiles_j, ntile, per, nsplit, tiles_n, ngroups;
+  int tiles_i, tiles_j, ntile, per, nsplit, tiles_n, ngroups, nv;
   int zbytes, xbytes;
   int8_t gy[LIC_MAX_TAPS], gx[LIC_MAX_TAPS];  // halo origin (dymin, dxmin) of each tap group
   int8_t ty[LIC_MAX_TAPS], tx[LIC_MAX_TAPS];  // tap offset inside its group's halo
 };
 
-template <int S, int G> struct WtrCfg {
+// NV > 1 (1x1 only): the work-group takes NV 64-channel blocks of ci and each wave treats them as
+// NV "virtual taps" (x plane pairs), so the dz fragment is again reused by NV MFMAs
+template <int S, int G, int NV = 1> struct WtrCfg {
   static constexpr int SPY = G == 9 ? 2 : 0;               // tap-window spans the halo covers
   static constexpr int SPX = G == 9 ? 2 : (G == 1 ? 0 : G - 1);
-  static constexpr int TI = G == 1 ? 16 : 8, TJ = 8;       // lattice tile (K per stage = TI*TJ)
+  static constexpr int TI = (G == 1 && NV == 1) ? 16 : 8, TJ = 8;   // lattice tile (K per stage = TI*TJ)
   static constexpr int HR = (TI - 1) * S + SPY + 1, HC = (TJ - 1) * S + SPX + 1;
   static constexpr int HPIX = HR * HC, ZPIX = TI * TJ;
-  static constexpr int ZB = 2 * ZPIX * 64, XB = 2 * HPIX * 64, BUF = ZB + XB;
+  static constexpr int NA = G * NV;                         // accumulator tiles per wave
+  static constexpr int ZB = 2 * ZPIX * 64, XB = 2 * NV * HPIX * 64, BUF = ZB + XB;
   static constexpr int LDS = 2 * BUF;
 };
 
@@ -53,12 +56,14 @@ __device__ __forceinline__ u32x4 tr_frag(const char* p, int d) {
   return r;
 }
 
-template <typename T, int S, int G, int PRO>
+template <typename T, int S, int G, int PRO, int NV = 1>
 __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a, const WtrPlan p,
                                                           float* __restrict__ ws) {
-  using C = WtrCfg<S, G>;
-  constexpr int TI = C::TI, TJ = C::TJ, HC = C::HC, HPIX = C::HPIX, ZPIX = C::ZPIX;
-  constexpr int ZU = ZPIX * 8 / 256, XU = (HPIX * 8 + 255) / 256;
+  static_assert(NV == 1 || G == 1, "virtual ci taps are for 1x1 windows");
+  using C = WtrCfg<S, G, NV>;
+  constexpr int TI = C::TI, TJ = C::TJ, HC = C::HC, HPIX = C::HPIX, ZPIX = C::ZPIX, NA = C::NA;
+  constexpr int XCH = 8 * NV;   // 16-byte chunks per halo pixel
+  constexpr int ZU = ZPIX * 8 / 256, XU = (HPIX * XCH + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -67,7 +72,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
   const int grp = bx % p.ngroups;
   bx /= p.ngroups;
   const int tn = bx % p.tiles_n, tm = bx / p.tiles_n;
-  const int n0 = tm * 64, c0 = tn * 64;
+  const int n0 = tm * 64, c0 = tn * 64 * NV;
   const int kbeg = blockIdx.y * p.per, kend = min(p.ntile, kbeg + p.per);
   const int gdy = p.gy[grp], gdx = p.gx[grp];
   const int tpi = p.tiles_i * p.tiles_j;
@@ -91,10 +96,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
     const int y0 = ti0 * S + gdy, x0 = tj0 * S + gdx;
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
-      const int c = tid + 256 * u, hp = c >> 3, ch = c0 + (c & 7) * 8;
+      const int c = tid + 256 * u, hp = c / XCH, ch = c0 + (c - hp * XCH) * 8;
       const int hr = hp / HC, hc = hp - hr * HC;
       const int y = y0 + hr, x = x0 + hc;
-      const bool ok = c < HPIX * 8 && (unsigned)y < (unsigned)a.h && (unsigned)x < (unsigned)a.w && ch < a.ci;
+      const bool ok = c < HPIX * XCH && (unsigned)y < (unsigned)a.h && (unsigned)x < (unsigned)a.w && ch < a.ci;
       const int off = ok ? (((b * a.h + y) * a.w + x) * a.ldx + ch) * 2 : OOB;
       xr[u] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
     }
@@ -109,8 +114,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
     }
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
-      const int c = tid + 256 * u, hp = c >> 3, cc = c & 7;
-      if (XU * 256 > HPIX * 8 && c >= HPIX * 8) continue;
+      const int c = tid + 256 * u, hp = c / XCH, cc = c - hp * XCH;
+      if (XU * 256 > HPIX * XCH && c >= HPIX * XCH) continue;
       u32x4 v = xr[u];
       if constexpr (PRO == LIC_PRO_SQUARE) {
         T* e = (T*)&v;
@@ -124,9 +129,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
     }
   };
 
-  floatx16 acc[G];
+  floatx16 acc[NA];
 #pragma unroll
-  for (int t = 0; t < G; ++t)
+  for (int t = 0; t < NA; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
@@ -135,9 +140,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
   const int col_b = (16 * g1 + 4 * pp) * 2;
   const int a_lane = wm * (ZPIX * 64) + (8 * hi + q) * 64 + col_b;
   const int b_lane = C::ZB + wn * (HPIX * 64) + (hi * S * HC + q * S) * 64 + col_b;
-  int toff[G];
+  int toff[NA];   // a tap's (or virtual tap's x plane pair's) byte offset into the halo image
 #pragma unroll
-  for (int t = 0; t < G; ++t) toff[t] = (p.ty[grp * G + t] * HC + p.tx[grp * G + t]) * 64;
+  for (int t = 0; t < NA; ++t) toff[t] = NV > 1 ? t * 2 * HPIX * 64 : (p.ty[grp * G + t] * HC + p.tx[grp * G + t]) * 64;
 
   auto compute = [&](int buf) {
     const char* za = smem + buf * C::BUF + a_lane;
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
     for (int s = 0; s < TI / 2; ++s) {
       const u32x4 fa = tr_frag(za + 16 * s * 64, 4 * 64);
 #pragma unroll
-      for (int t = 0; t < G; ++t) {
+      for (int t = 0; t < NA; ++t) {
         const u32x4 fb = tr_frag(xbb + toff[t] + 2 * s * S * HC * 64, 4 * S * 64);
         acc[t] = mfma_k16<T>(fa, fb, acc[t]);
       }
@@ -168,10 +173,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
   }
 
   // partial tile -> ws[split][tap][co][ci] (lanes 0..31 write 32 consecutive ci)
-  const int col = c0 + wn * 32 + (lane & 31);
 #pragma unroll
-  for (int t = 0; t < G; ++t) {
-    float* out = ws + ((int64_t)blockIdx.y * a.ntaps + grp * G + t) * a.co * a.ci;
+  for (int t = 0; t < NA; ++t) {
+    const int col = c0 + (NV > 1 ? t * 64 : 0) + wn * 32 + (lane & 31);
+    float* out = ws + ((int64_t)blockIdx.y * a.ntaps + (NV > 1 ? 0 : grp * G + t)) * a.co * a.ci;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = n0 + wm * 32 + 8 * (r >> 2) + 4 * hi + (r & 3);
@@ -217,11 +222,15 @@ static int wtr_plan(const lic_wgrad_args& a, WtrPlan& p) {
   if (zb >= ((int64_t)1 << 31) || xb >= ((int64_t)1 << 31)) return 0;
   p.zbytes = (int)zb;
   p.xbytes = (int)xb;
-  const int TI = G == 1 ? 16 : 8;
+  // 1x1 at stride 1: NV ci blocks per work-group (NV divides the block count where it can)
+  const int nb = (a.ci + 63) / 64;
+  p.nv = 1;
+  if (G == 1 && a.isy == 1 && nb > 1) p.nv = nb <= 4 ? nb : (nb % 4 == 0 ? 4 : (nb % 3 == 0 ? 3 : (nb % 2 == 0 ? 2 : 4)));
+  const int TI = (G == 1 && p.nv == 1) ? 16 : 8;
   p.tiles_i = (a.mi + TI - 1) / TI;
   p.tiles_j = (a.mj + 7) / 8;
   p.ntile = a.n * p.tiles_i * p.tiles_j;
-  p.tiles_n = (a.ci + 63) / 64;
+  p.tiles_n = (nb + p.nv - 1) / p.nv;
   const int blocks = ((a.co + 63) / 64) * p.tiles_n * p.ngroups;
   // ~512 work-groups (two per CU), at least 8 tiles each (the partials stay well below the operands)
   int ns = (512 + blocks - 1) / blocks;
@@ -236,10 +245,11 @@ int wgrad_tr_nsplit(const lic_wgrad_args& a) {
   return wtr_plan(a, p) ? p.nsplit : 0;
 }
 
-template <typename T, int S, int G>
+template <typename T, int S, int G, int NV = 1>
 static int wtr_launch(const lic_wgrad_args& a, const WtrPlan& p, hipStream_t s) {
-  using C = WtrCfg<S, G>;
-  auto kern = a.prologue == LIC_PRO_SQUARE ? wgrad_tr_kernel<T, S, G, LIC_PRO_SQUARE> : wgrad_tr_kernel<T, S, G, LIC_PRO_NONE>;
+  using C = WtrCfg<S, G, NV>;
+  auto kern = a.prologue == LIC_PRO_SQUARE ? wgrad_tr_kernel<T, S, G, LIC_PRO_SQUARE, NV>
+                                           : wgrad_tr_kernel<T, S, G, LIC_PRO_NONE, NV>;
   if (C::LDS > 64 * 1024) {
     const hipError_t e = ensure_dyn_lds((const void*)kern, C::LDS);
     if (e != hipSuccess) return fail(std::string("wgrad: dynamic LDS: ") + hipGetErrorString(e));
@@ -256,6 +266,9 @@ static int wtr_launch_t(const lic_wgrad_args& a, const WtrPlan& p, int G, hipStr
     if (G == 9) return wtr_launch<T, 1, 9>(a, p, s);
     if (G == 5) return wtr_launch<T, 1, 5>(a, p, s);
     if (G == 7) return wtr_launch<T, 1, 7>(a, p, s);
+    if (p.nv == 4) return wtr_launch<T, 1, 1, 4>(a, p, s);
+    if (p.nv == 3) return wtr_launch<T, 1, 1, 3>(a, p, s);
+    if (p.nv == 2) return wtr_launch<T, 1, 1, 2>(a, p, s);
     return wtr_launch<T, 1, 1>(a, p, s);
   }
   if (G == 9) return wtr_launch<T, 2, 9>(a, p, s);

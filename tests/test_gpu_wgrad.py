@@ -31,6 +31,9 @@ def _check(dw, ref, name):
     (1, 16, 16, 192, 128, 3, 1, (1, 1, 1, 1)),     # 3 x 2 channel blocks
     (2, 12, 10, 96, 40, 3, 1, (1, 1, 1, 1)),       # partial 64-wide blocks on both sides
     (2, 18, 14, 32, 96, 1, 1, (0, 0, 0, 0)),       # 1x1 (16 x 8 tiles)
+    (2, 18, 14, 128, 64, 1, 1, (0, 0, 0, 0)),      # 1x1, two ci blocks as virtual taps
+    (1, 20, 12, 320, 96, 1, 1, (0, 0, 0, 0)),      # 1x1, 5 ci blocks -> 4 + 1 (partial group)
+    (1, 16, 16, 256, 192, 1, 1, (0, 0, 0, 0)),     # 1x1, 4 virtual taps
     (2, 16, 16, 32, 64, 5, 2, (1, 1, 2, 2)),       # ZeroPad2d((1, 2, 1, 2)) + conv5x5 s2
     (2, 17, 15, 64, 64, 3, 2, (1, 1, 1, 1)),       # conv3x3 s2, odd map
     (1, 12, 12, 64, 32, 5, 1, (2, 2, 2, 2)),       # 5x5 s1 (rows of 5 taps)
