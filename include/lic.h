@@ -356,6 +356,8 @@ typedef struct lic_wgrad_args {
   float* dw; int64_t s_co, s_ci, s_tap;          /* fp32 destination + element strides */
   int32_t co_out, ci_out, accumulate;
   float* ws; int64_t ws_bytes;
+  float* db;           /* optional (NULL: none): fp32 bias gradient, db[n] (+)= sum of dz[., n] over the
+                          lattice, n < co_out (accumulate as dw); the lattice must be dz's full map (abi 4) */
 } lic_wgrad_args;
 int64_t lic_conv2d_wgrad_workspace(const lic_wgrad_args* a);   /* bytes, -1 on bad args */
 int lic_conv2d_wgrad(const lic_wgrad_args* a, lic_stream_t stream);

@@ -112,6 +112,7 @@ class WgradArgs(ctypes.Structure):
         ("dw", _vp), ("s_co", ctypes.c_int64), ("s_ci", ctypes.c_int64), ("s_tap", ctypes.c_int64),
         ("co_out", _i32), ("ci_out", _i32), ("accumulate", _i32),
         ("ws", _vp), ("ws_bytes", ctypes.c_int64),
+        ("db", _vp),
     ]
 
 

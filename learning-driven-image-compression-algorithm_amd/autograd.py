@@ -62,9 +62,11 @@ def _taps(kh, kw, pt, pl):
 # --------------------------------------------------------------------------- primitives
 def wgrad(x: torch.Tensor, dz: torch.Tensor, dy: Sequence[int], dx: Sequence[int], *, stride: int = 1,
           lattice: Optional[Tuple[int, int]] = None, dw: torch.Tensor, strides: Tuple[int, int, int],
-          co_out: int, ci_out: int, prologue: int = PRO_NONE, accumulate: bool = False) -> torch.Tensor:
+          co_out: int, ci_out: int, prologue: int = PRO_NONE, accumulate: bool = False,
+          db: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dw[n*s_co + c*s_ci + t*s_tap] (+)= sum_pix dz[pix, n] * pro(x[pix*stride + tap_t, c]).
-    x, dz: NHWC with 16-byte channel counts; lattice = (mi, mj) output pixels (default dz's map)."""
+    x, dz: NHWC with 16-byte channel counts; lattice = (mi, mj) output pixels (default dz's map).
+    db (fp32 [co_out], optional): the bias gradient sum_pix dz[pix, n] from the same launch."""
     if x.dtype != dz.dtype:
         raise ValueError("wgrad: x and dz dtypes differ")
     if dw.dtype != torch.float32 or not dw.is_contiguous():
@@ -86,6 +88,10 @@ def wgrad(x: torch.Tensor, dz: torch.Tensor, dy: Sequence[int], dx: Sequence[int
     a.dw = _dp(dw)
     a.s_co, a.s_ci, a.s_tap = strides
     a.co_out, a.ci_out, a.accumulate = co_out, ci_out, 1 if accumulate else 0
+    if db is not None:
+        if db.dtype != torch.float32 or not db.is_contiguous() or db.numel() < co_out:
+            raise ValueError("wgrad: db must be contiguous fp32 with co_out elements")
+        a.db = _dp(db)
     need = int(_lib().lic_conv2d_wgrad_workspace(ctypes.byref(a)))
     if need < 0:
         check(_lib().lic_conv2d_wgrad(ctypes.byref(a), stream_handle()))  # raises with the reason
@@ -196,13 +202,16 @@ class _Conv2dFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _conv_dgrad(dzp, weight, stride, pad, H, W)
+        want_db = has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             dw = torch.empty((co, ci, kh, kw), dtype=torch.float32, device=dz.device)
             tdy, tdx = _taps(kh, kw, pad[0], pad[1])
+            # the bias gradient comes out of the same launch (column sums of the staged dz tiles)
+            db = torch.empty((co,), dtype=torch.float32, device=dz.device) if want_db else None
             wgrad(xp, dzp, tdy, tdx, stride=stride, dw=dw, strides=(ci * kh * kw, kh * kw, 1), co_out=co,
-                  ci_out=ci)
+                  ci_out=ci, db=db)
             dw = dw.to(weight.dtype)
-        if has_bias and ctx.needs_input_grad[2]:
+        if want_db and db is None:
             db = channel_sum(dz)
         return dx, dw, db, None, None, None, None
 

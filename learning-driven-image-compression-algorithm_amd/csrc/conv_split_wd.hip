@@ -462,7 +462,7 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2>(a, s, status);
     if (a.ntaps == 9) return try_split_wd<2, 9, 8, 8, 32, 2, 1, 4>(a, s, status);
   }
-  if (a.mi >= 8 && a.mj >= 8 && blocks(16, 16, 64) < 256 && blocks(8, 8, 64) >= 64) {
+  if (a.mi >= 8 && a.mj >= 8 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8) && blocks(8, 8, 64) >= 64) {
     if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
     if (a.ntaps == 9) return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);
   }

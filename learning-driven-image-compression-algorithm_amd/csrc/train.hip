@@ -202,12 +202,26 @@ __global__ __launch_bounds__(WM * WN * 64) void wgrad_kernel(const lic_wgrad_arg
     }
 }
 
+// dw = sum over the splits; with wsb (tiled kernel's per-split bias sums [nsplit][co]) the threads
+// past the weight elements also finish db[n], n < co_out
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, int ntaps, int co, int ci, int co_out,
                                     int ci_out, float* __restrict__ dw, int64_t s_co, int64_t s_ci, int64_t s_tap,
-                                    int accumulate) {
+                                    int accumulate, const float* __restrict__ wsb, float* __restrict__ db) {
   const int64_t total = (int64_t)ntaps * co_out * ci_out;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total) return;
+  if (idx >= total) {
+    const int n = (int)(idx - total);
+    if (!wsb || n >= co_out) return;
+    float b0 = 0.f, b1 = 0.f;
+    int k = 0;
+    for (; k + 2 <= nsplit; k += 2) {
+      b0 += wsb[(int64_t)k * co + n];
+      b1 += wsb[(int64_t)(k + 1) * co + n];
+    }
+    if (k < nsplit) b0 += wsb[(int64_t)k * co + n];
+    db[n] = accumulate ? db[n] + (b0 + b1) : b0 + b1;
+    return;
+  }
   const int c = (int)(idx % ci_out);
   const int64_t r = idx / ci_out;
   const int n = (int)(r % co_out);
@@ -264,6 +278,8 @@ static int wgrad_check(const lic_wgrad_args& a) {
   if (a.ntaps <= 0 || a.ntaps > LIC_MAX_TAPS) return fail("wgrad: ntaps out of range");
   if (a.ci_out > a.ci || a.co_out > a.co || a.ci_out <= 0 || a.co_out <= 0) return fail("wgrad: bad ci_out / co_out");
   if (a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE) return fail("wgrad: prologue must be NONE or SQUARE");
+  if (a.db && (a.oy0 || a.ox0 || a.osy != 1 || a.osx != 1 || a.mi != a.ho || a.mj != a.wo))
+    return fail("wgrad: db needs the lattice to be dz's full map");
   // lattice bounds (host-side shape check: every dz read is in range)
   if (a.oy0 + a.osy * (a.mi - 1) >= a.ho || a.ox0 + a.osx * (a.mj - 1) >= a.wo || a.oy0 < 0 || a.ox0 < 0)
     return fail("wgrad: output lattice exceeds the dz map");
@@ -953,11 +969,21 @@ int wgrad_tr_nsplit(const lic_wgrad_args& a);
 int wgrad_tr_launch(const lic_wgrad_args& a, hipStream_t s, int* nsplit);
 }  // namespace lic
 
+// workspace: [nsplit][tap][co][ci] fp32 partials, then (db requested) the bias partials: [nsplit][co]
+// for the tiled kernel, the channel-sum parts [CS_CHUNKS][co] otherwise
+static int64_t wgrad_ws_bytes(const lic_wgrad_args& a, int* nsplit_out, bool* tiled_out) {
+  const int tr = wgrad_tr_nsplit(a);
+  const int ns = tr ? tr : wgrad_plan(a).nsplit;
+  if (nsplit_out) *nsplit_out = ns;
+  if (tiled_out) *tiled_out = tr != 0;
+  int64_t b = (int64_t)ns * a.ntaps * a.co * a.ci;
+  if (a.db) b += (int64_t)(tr ? ns : CS_CHUNKS) * a.co;
+  return b * (int64_t)sizeof(float);
+}
+
 extern "C" int64_t lic_conv2d_wgrad_workspace(const lic_wgrad_args* a) {
   if (!a || wgrad_check(*a)) return -1;
-  int ns = wgrad_tr_nsplit(*a);
-  if (!ns) ns = wgrad_plan(*a).nsplit;
-  return (int64_t)ns * a->ntaps * a->co * a->ci * (int64_t)sizeof(float);
+  return wgrad_ws_bytes(*a, nullptr, nullptr);
 }
 
 extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {
@@ -965,9 +991,10 @@ extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {
   const lic_wgrad_args& a = *ap;
   if (int e = wgrad_check(a)) return e;
   const WgPlan p = wgrad_plan(a);
-  const int tr_ns = wgrad_tr_nsplit(a);
-  const int nsplit = tr_ns ? tr_ns : p.nsplit;
-  const int64_t need = (int64_t)nsplit * a.ntaps * a.co * a.ci * (int64_t)sizeof(float);
+  int nsplit = 0;
+  bool tiled = false;
+  const int64_t need = wgrad_ws_bytes(a, &nsplit, &tiled);
+  const int tr_ns = tiled ? nsplit : 0;
   if (!a.ws || a.ws_bytes < need)
     return fail("wgrad: workspace too small (" + std::to_string(a.ws_bytes) + " < " + std::to_string(need) + ")");
   hipStream_t s = (hipStream_t)stream;
@@ -986,9 +1013,24 @@ extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {
   }
   LIC_CHECK_LAUNCH();
   const int64_t total = (int64_t)a.ntaps * a.co_out * a.ci_out;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(tr_nblk(total)), dim3(256), 0, s, a.ws, nsplit, a.ntaps, a.co, a.ci,
-                     a.co_out, a.ci_out, a.dw, a.s_co, a.s_ci, a.s_tap, a.accumulate);
+  float* const wsb = a.ws + (int64_t)nsplit * a.ntaps * a.co * a.ci;
+  const bool fused_db = a.db && tiled;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(tr_nblk(total + (fused_db ? a.co_out : 0))), dim3(256), 0, s, a.ws,
+                     nsplit, a.ntaps, a.co, a.ci, a.co_out, a.ci_out, a.dw, a.s_co, a.s_ci, a.s_tap, a.accumulate,
+                     fused_db ? wsb : nullptr, a.db);
   LIC_CHECK_LAUNCH();
+  if (a.db && !tiled) {   // generic kernel: the two-pass channel sum over dz
+    const int npix = a.n * a.ho * a.wo;
+    const int per = std::max(1, (npix + CS_CHUNKS - 1) / CS_CHUNKS);
+    const int nparts = std::max(1, (npix + per - 1) / per);
+    TR_DISPATCH(a.dtype, "wgrad db",
+                hipLaunchKernelGGL(channel_sum_partial_kernel<T>, dim3(nparts, (a.co_out + 63) / 64), dim3(256), 0, s,
+                                   (const T*)a.dz, a.ldz, npix, a.co_out, per, wsb));
+    LIC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(channel_sum_reduce_kernel, dim3((a.co_out + 63) / 64), dim3(1024), 0, s, wsb, nparts, a.co_out,
+                       a.db, a.accumulate);
+    LIC_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -19,7 +19,9 @@
 // row offset into the halo image, so the dz fragment is read once per K step and reused by all
 // G taps (G MFMAs per 2 + 2G transpose reads).  64-byte plane rows make each 32-lane half's
 // 4 rows x 64 B one conflict-free 256-byte span.  Partials go to ws[split][tap][co][ci] and
-// the deterministic wgrad_reduce_kernel (train.hip) sums the splits.
+// the deterministic wgrad_reduce_kernel (train.hip) sums the splits.  With a bias gradient requested,
+// the waves of the first ci block / tap group also sum their dz fragments (8 values per lane and K
+// step, VALU) into per-split column sums that the same reduce finishes: db costs no extra pass over dz.
 #include "lic_common.h"
 
 namespace lic {
@@ -58,7 +60,7 @@ __device__ __forceinline__ u32x4 tr_frag(const char* p, int d) {
 
 template <typename T, int S, int G, int PRO, int NV = 1>
 __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a, const WtrPlan p,
-                                                          float* __restrict__ ws) {
+                                                          float* __restrict__ ws, float* __restrict__ wsb) {
   static_assert(NV == 1 || G == 1, "virtual ci taps are for 1x1 windows");
   using C = WtrCfg<S, G, NV>;
   constexpr int TI = C::TI, TJ = C::TJ, HC = C::HC, HPIX = C::HPIX, ZPIX = C::ZPIX, NA = C::NA;
@@ -144,12 +146,20 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
 #pragma unroll
   for (int t = 0; t < NA; ++t) toff[t] = NV > 1 ? t * 2 * HPIX * 64 : (p.ty[grp * G + t] * HC + p.tx[grp * G + t]) * 64;
 
+  // bias partial: lane l sums dz[k][co = n0 + 32 wm + (l & 31)] over its K half (wave-uniform branch)
+  const bool do_bias = wsb != nullptr && tn == 0 && grp == 0 && wn == 0;
+  float bsum = 0.f;
   auto compute = [&](int buf) {
     const char* za = smem + buf * C::BUF + a_lane;
     const char* xbb = smem + buf * C::BUF + b_lane;
 #pragma unroll
     for (int s = 0; s < TI / 2; ++s) {
       const u32x4 fa = tr_frag(za + 16 * s * 64, 4 * 64);
+      if (do_bias) {
+        const T* e = (const T*)&fa;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bsum += to_f(e[q]);
+      }
 #pragma unroll
       for (int t = 0; t < NA; ++t) {
         const u32x4 fb = tr_frag(xbb + toff[t] + 2 * s * S * HC * 64, 4 * S * 64);
@@ -172,6 +182,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
     }
   }
 
+  if (do_bias) {
+    bsum += __shfl_xor(bsum, 32);
+    const int co = n0 + wm * 32 + lane;
+    if (lane < 32 && co < a.co) wsb[(int64_t)blockIdx.y * a.co + co] = bsum;
+  }
   // partial tile -> ws[split][tap][co][ci] (lanes 0..31 write 32 consecutive ci)
 #pragma unroll
   for (int t = 0; t < NA; ++t) {
@@ -255,7 +270,8 @@ static int wtr_launch(const lic_wgrad_args& a, const WtrPlan& p, hipStream_t s) 
     if (e != hipSuccess) return fail(std::string("wgrad: dynamic LDS: ") + hipGetErrorString(e));
   }
   const dim3 grid(((a.co + 63) / 64) * p.tiles_n * p.ngroups, p.nsplit);
-  hipLaunchKernelGGL(kern, grid, dim3(256), C::LDS, s, a, p, a.ws);
+  float* wsb = a.db ? a.ws + (int64_t)p.nsplit * a.ntaps * a.co * a.ci : nullptr;
+  hipLaunchKernelGGL(kern, grid, dim3(256), C::LDS, s, a, p, a.ws, wsb);
   LIC_CHECK_LAUNCH();
   return 0;
 }

@@ -380,16 +380,20 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
          force_direct: bool = False, force_generic: bool = False) -> Act:
     """Run one ConvPack launch. For convT phases `out` (full map) must be given."""
     if (split_mode() == 2 and x.dtype == torch.float32 and not (force_direct or force_generic or shuffle) and
-            act == _ffi.ACT_NONE and epi == _ffi.EPI_PLAIN and r1 is None and g is None and r2 is None and
+            epi == _ffi.EPI_PLAIN and r1 is None and g is None and r2 is None and
             y2 is None and x.B * x.H * x.W >= 65536):
         phases = stride2_phase_packs(pk)
-        if phases is not None:
+        if phases is not None and len(phases) > 1:
             # fp32x6 stride-2 k x k conv as its four input-parity phases, accumulated in fp32 through
-            # the epilogue's residual operand (the first phase adds the bias)
+            # the epilogue's residual operand (the first phase adds the bias); an activation goes on
+            # the last phase as RES_ACT, act(acc + b + r1): the same fp32 sum, then the activation
             hw = out_hw if out_hw is not None else conv_out_hw(x.H, x.W, pk)
             out = conv(x, phases[0], out, prologue=prologue, out_hw=hw)
-            for ph in phases[1:]:
-                conv(x, ph, out, r1=out, prologue=prologue, out_hw=hw)
+            for k, ph in enumerate(phases[1:]):
+                last = k == len(phases) - 2
+                conv(x, ph, out, r1=out, prologue=prologue, out_hw=hw,
+                     act=act if last else _ffi.ACT_NONE, slope=slope,
+                     epi=_ffi.EPI_RES_ACT if (last and act != _ffi.ACT_NONE) else _ffi.EPI_PLAIN)
             return out
     if x.c != pk.ci:
         raise ValueError(f"conv: input has {x.c} channels, weights expect {pk.ci}")

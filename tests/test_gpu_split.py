@@ -37,6 +37,8 @@ DEV = "cuda"
     (224, 128, 3, 1, (1, 1, 1, 1), 32, 16, "plain"),   # slice-loop cc transform (8x8 px x 64 ch tiles)
     (192, 192, 3, 2, (1, 1, 1, 1), 32, 64, "plain"),   # ResidualBlockWithStride conv3x3 s2: 4/2/2/1-tap phases
     (128, 32, 3, 1, (1, 1, 1, 1), 32, 16, "plain"),    # per-slice 32-channel head (8x8 px x 32 ch tiles)
+    (192, 192, 3, 2, (1, 1, 1, 1), 32, 64, "gelu"),    # stride-2 phases, activation on the last phase
+    (256, 1152, 3, 1, (1, 1, 1, 1), 32, 8, "plain"),   # h_s 8x8 map: 8x8 px x 64 ch tiles
     (224, 24, 3, 1, (1, 1, 1, 1), 8, 20, "gelu"),      # copad 32 with 8 masked channels, ragged map
     (128, 32, 1, 1, (0, 0, 0, 0), 32, 16, "plain"),    # 32-channel 1x1 on virtual taps
 ])
