@@ -82,12 +82,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="informational; world size comes from torchrun")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole step (forward, backward, clip, Adam) in one hipGraph and replay it: "
-                         "no per-launch host cost; the noise seed lives on the device (bf16 / fp32, one GPU)")
+                         "no per-launch host cost; the noise seed lives on the device (bf16 / fp32, one GPU; "
+                         "the default there)")
+    ap.add_argument("--eager", action="store_true", help="run every step eagerly (no hipGraph capture)")
     args = ap.parse_args()
 
     from lic_amd import distributed as D
     from lic_amd.model import net_ga, net_unet_ha_hs
     rank, world, local = D.init("nccl")
+    # one GPU, bf16 / fp32: the captured step is the default (replays equal the eager steps,
+    # tests/test_gpu_train_net.py::test_train_step_hipgraph_matches_eager); ~7000 launches per step
+    # otherwise leave the GPU waiting on the host
+    args.graph = not args.eager and (args.graph or (world == 1 and args.precision != "fp16"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B = int(args.batch_size)
@@ -189,7 +195,8 @@ def main():
                 "data": "synthetic (seeded smooth images, random crops in HBM; no DIV2K)",
                 "config": {"workload": f"{args.arch} Net.forward(x,'train') + backward + grad all-reduce + clip + Adam",
                            "global_batch": world * B, "crop": args.crop, "lambda": args.lmbda,
-                           "parallelism": f"data-parallel x{world} (bucketed RCCL all-reduce)"},
+                           "parallelism": f"data-parallel x{world} (bucketed RCCL all-reduce)",
+                           "execution": "hipGraph replay of the whole step" if args.graph else "eager"},
                 "loss_first_last": [round(first, 4), round(last, 4)]}), flush=True)
         D.finish(world)
         return
