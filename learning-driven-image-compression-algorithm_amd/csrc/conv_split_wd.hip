@@ -53,6 +53,7 @@ struct WdPlan {
                              // input stride 2 (a stride-2 conv's phase, conv.hip), else 1
   int rp_off;                // byte offset of rowpix[BM] + bias[BN]
   int nchunks;
+  int ncb;                   // > 0: XCD-aware 1-D grid of (tile, channel block) pairs, ncb channel blocks
 };
 
 // VT > 0: a 1x1 convolution whose NTAPS = VT "virtual taps" are VT consecutive 16-channel chunks
@@ -93,12 +94,20 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31, lhalf = lane >> 5;
 
-  int bid = blockIdx.x;
+  // XCD-aware order (p.ncb > 0): workgroups are dealt round-robin to the 8 XCDs, so id, id + 8, ...
+  // share an L2; they take the ncb channel blocks of one tile in turn, and the halo each block
+  // re-reads is then an L2 hit instead of a second trip to HBM
+  int bid = blockIdx.x, cb = blockIdx.y;
+  if (p.ncb > 0) {
+    const int q = (int)blockIdx.x >> 3, t8 = q / p.ncb;
+    cb = q - t8 * p.ncb;
+    bid = t8 * 8 + ((int)blockIdx.x & 7);
+  }
   const int tx_t = bid % p.tiles_x;
   bid /= p.tiles_x;
   const int ty_t = bid % p.tiles_y;
   const int b = bid / p.tiles_y;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = cb * BN;
   const int i0 = ty_t * TH, j0 = tx_t * TW;
   const int iy0 = i0 * a.isy + p.dymin, ix0 = j0 * a.isx + p.dxmin;
 
@@ -428,7 +437,13 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   const int smem = p.rp_off + tail;
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   if ((int64_t)(a.copad / 32) * p.nchunks * NTAPS * SplitMode<MODE>::NPB * 1024 >= (1LL << 31)) return 0;
-  dim3 grid((unsigned)blocks, (a.copad + BN - 1) / BN);
+  const int ncb = (a.copad + BN - 1) / BN;
+  static const bool remap_on = [] {
+    const char* e = getenv("LIC_WD_XCD");
+    return !(e && e[0] == '0');
+  }();
+  p.ncb = (remap_on && ncb > 1 && blocks % 8 == 0) ? ncb : 0;
+  dim3 grid = p.ncb ? dim3((unsigned)(blocks * ncb), 1) : dim3((unsigned)blocks, ncb);
   auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
