@@ -479,13 +479,33 @@ int lic_dwconv_wgrad(int32_t dtype, const void* x, int32_t ldx, const void* dz, 
                      int32_t ntaps, const int8_t* dy, const int8_t* dx, float* dw, float* ws,
                      int64_t ws_bytes, lic_stream_t stream);
 
+/* compressai AttentionBlock ResidualUnit(N) in one launch, fp32 activations with fp32x6 split
+ * products (mfma_mode 2):  y = relu(conv1x1_{N/2->N}(relu(conv3x3_{N/2->N/2}(relu(conv1x1_{N->N/2}(x)))))
+ * + x), conv3x3 zero-padded by 1.  Replaces the three lic_conv2d_fwd launches of one ResidualUnit
+ * (compressai layers.py AttentionBlock.ResidualUnit; SWAtten conv_a / conv_b at net_ga.py:118-136,
+ * 6 per SWAtten).  w1s / w2s / w3s are the three convs' fp32x6 split packs in MFMA-fragment order
+ * (lic_conv_args.wgt_split: conv[0] copad N/2 cpad N 1 tap, conv[2] copad N/2 cpad N/2 9 taps
+ * row-major (dy, dx) = (-1..1, -1..1), conv[4] copad N cpad N/2 1 tap); b1 / b2 / b3 fp32 biases.
+ * N = 128; h, w multiples of 8; x != y; views, weights and biases 16-B aligned (abi 5). */
+typedef struct lic_resunit_args {
+  int32_t dtype;                       /* LIC_F32 */
+  const void* x; int32_t n, h, w, c, ldx;
+  void* y; int32_t ldy;
+  const void* w1s; const void* w2s; const void* w3s;
+  const float* b1; const float* b2; const float* b3;
+  int32_t mfma_mode;                   /* 2 */
+} lic_resunit_args;
+int lic_resunit_fwd(const lic_resunit_args* a, lic_stream_t stream);
+
 /* Library info.
  * LIC_ABI_VERSION changes whenever an entry point's parameter list or an args struct's layout
- * changes (3: lic_conv_args.mfma_mode / wgt_split, lic_rate_train_* seed_dev / seed_mul).  A
+ * changes (3: lic_conv_args.mfma_mode / wgt_split, lic_rate_train_* seed_dev / seed_mul; 5:
+ * lic_resunit_args / lic_resunit_fwd).  A
  * caller compiled against this header checks lic_abi_version() == LIC_ABI_VERSION and
  * lic_args_size(k) == sizeof(...) once after loading the library (the Python host does, _ffi.load). */
-#define LIC_ABI_VERSION 4
-enum { LIC_ARGS_CONV = 0, LIC_ARGS_ATTN = 1, LIC_ARGS_RATE = 2, LIC_ARGS_RANS = 3, LIC_ARGS_WGRAD = 4 };
+#define LIC_ABI_VERSION 5
+enum { LIC_ARGS_CONV = 0, LIC_ARGS_ATTN = 1, LIC_ARGS_RATE = 2, LIC_ARGS_RANS = 3, LIC_ARGS_WGRAD = 4,
+       LIC_ARGS_RESUNIT = 5 };
 const char* lic_last_error(void);
 const char* lic_version(void);
 int32_t lic_abi_version(void);

@@ -18,7 +18,7 @@ ACT_NONE, ACT_RELU, ACT_LRELU, ACT_GELU, ACT_ROUND = 0, 1, 2, 3, 4
 PRO_NONE, PRO_SQUARE, PRO_ABS = 0, 1, 2
 EPI_PLAIN, EPI_GATE, EPI_HALF_TANH, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, EPI_RES_ACT = 0, 1, 2, 3, 4, 5, 6
 MAX_TAPS = 64
-ABI_VERSION = 4   # include/lic.h LIC_ABI_VERSION
+ABI_VERSION = 5   # include/lic.h LIC_ABI_VERSION
 
 EXPORTED_SYMBOLS = (
     "lic_conv2d_fwd", "lic_gdn_prepare", "lic_win_attn_fwd", "lic_layernorm_fwd",
@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "lic_layernorm_bwd", "lic_gate_fwd", "lic_half_tanh_fwd", "lic_half_tanh_bwd", "lic_avgpool_bwd",
     "lic_rate_train_parts", "lic_rate_train_fwd", "lic_rate_train_bwd", "lic_recon_train_blocks",
     "lic_recon_train_fwd", "lic_recon_train_bwd", "lic_dwconv_wgrad_workspace", "lic_dwconv_wgrad",
+    "lic_resunit_fwd",
 )
 LIC_EB_PARAMS = 58
 
@@ -113,6 +114,17 @@ class WgradArgs(ctypes.Structure):
         ("co_out", _i32), ("ci_out", _i32), ("accumulate", _i32),
         ("ws", _vp), ("ws_bytes", ctypes.c_int64),
         ("db", _vp),
+    ]
+
+
+class ResunitArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i32),
+        ("x", _vp), ("n", _i32), ("h", _i32), ("w", _i32), ("c", _i32), ("ldx", _i32),
+        ("y", _vp), ("ldy", _i32),
+        ("w1s", _vp), ("w2s", _vp), ("w3s", _vp),
+        ("b1", _vp), ("b2", _vp), ("b3", _vp),
+        ("mfma_mode", _i32),
     ]
 
 
@@ -204,6 +216,7 @@ def load():
         "lic_recon_train_fwd": [I, V, I, I, I, I, V, I, V, V, V, V],
         "lic_recon_train_bwd": [I, V, I, I, I, I, V, I, V, V, F, V, I, V, V, L, V],
         "lic_dwconv_wgrad": [I, V, I, V, I, I, I, I, I, I, I, I, I, V, V, V, V, L, V],
+        "lic_resunit_fwd": [V, V],
     }
     for name, argt in sig.items():
         fn = getattr(lib, name)
@@ -233,7 +246,7 @@ def load():
     if abi != ABI_VERSION:
         _load_error = f"liblic ABI {abi} at {path}, this host expects {ABI_VERSION}: rebuild liblic.so"
         raise LicError(_load_error)
-    for which, st in enumerate((ConvArgs, AttnArgs, RateArgs, RansArgs, WgradArgs)):
+    for which, st in enumerate((ConvArgs, AttnArgs, RateArgs, RansArgs, WgradArgs, ResunitArgs)):
         if lib.lic_args_size(which) != ctypes.sizeof(st):
             _load_error = (f"liblic args struct {st.__name__}: library {lib.lic_args_size(which)} bytes, "
                            f"host {ctypes.sizeof(st)}: rebuild liblic.so")

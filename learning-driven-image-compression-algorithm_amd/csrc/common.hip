@@ -29,7 +29,7 @@ hipError_t ensure_dyn_lds(const void* kern, int bytes) {
 }  // namespace lic
 
 extern "C" const char* lic_last_error(void) { return lic::g_err.c_str(); }
-extern "C" const char* lic_version(void) { return "liblic 0.4 gfx950 (abi 4)"; }
+extern "C" const char* lic_version(void) { return "liblic 0.5 gfx950 (abi 5)"; }
 extern "C" int32_t lic_abi_version(void) { return LIC_ABI_VERSION; }
 extern "C" int64_t lic_args_size(int32_t which) {
   switch (which) {
@@ -38,6 +38,7 @@ extern "C" int64_t lic_args_size(int32_t which) {
     case LIC_ARGS_RATE: return (int64_t)sizeof(lic_rate_args);
     case LIC_ARGS_RANS: return (int64_t)sizeof(lic_rans_args);
     case LIC_ARGS_WGRAD: return (int64_t)sizeof(lic_wgrad_args);
+    case LIC_ARGS_RESUNIT: return (int64_t)sizeof(lic_resunit_args);
     default: return -1;
   }
 }

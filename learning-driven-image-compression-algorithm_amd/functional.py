@@ -449,6 +449,49 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     return out
 
 
+_TAPS3 = ([-1, -1, -1, 0, 0, 0, 1, 1, 1], [-1, 0, 1, -1, 0, 1, -1, 0, 1])
+
+
+def resunit_fusable(x: Act, p1: ConvPack, p2: ConvPack, p3: ConvPack, out: Optional[Act] = None) -> bool:
+    """True when the fused fp32x6 ResidualUnit kernel (lic_resunit_fwd) takes this call: the calling
+    thread is in fp32x6 mode, fp32 activations, N = 128, an 8-aligned map, aligned views, the
+    three packs are conv1x1 N->N/2, conv3x3 (pad 1) N/2->N/2, conv1x1 N/2->N, and out is not x."""
+    N = x.c
+    if split_mode() != 2 or x.dtype != torch.float32 or N != 128 or x.H % 8 or x.W % 8:
+        return False
+    if x.ld % 4 or x.ptr % 16 or (out is not None and (out.ld % 4 or out.ptr % 16 or out.t.data_ptr() == x.t.data_ptr())):
+        return False
+    geo = ((p1, N, N // 2, 1), (p2, N // 2, N // 2, 9), (p3, N // 2, N, 1))
+    for pk, ci, co, nt in geo:
+        if (pk.groups != 1 or pk.stride != 1 or pk.phase is not None or pk.ci != ci or pk.co != co or
+                pk.copad != co or pk.cpad != ci or len(pk.dy) != nt or pk.bias is None or pk.w.dtype != torch.float32 or
+                pk.bias.data_ptr() % 16):
+            return False
+    return list(p1.dy) == [0] and list(p1.dx) == [0] and list(p3.dy) == [0] and list(p3.dx) == [0] and \
+        list(p2.dy) == _TAPS3[0] and list(p2.dx) == _TAPS3[1]
+
+
+def resunit(x: Act, p1: ConvPack, p2: ConvPack, p3: ConvPack, out: Optional[Act] = None) -> Act:
+    """compressai ResidualUnit relu(conv1x1(relu(conv3x3(relu(conv1x1(x))))) + x) in one fp32x6
+    launch (csrc/resunit_split.hip); callers check resunit_fusable first."""
+    if not resunit_fusable(x, p1, p2, p3, out):
+        raise ValueError("resunit: this call is not supported by the fused kernel (see resunit_fusable)")
+    ws = [split_weights(pk, 2) for pk in (p1, p2, p3)]
+    if any(w is None for w in ws):
+        raise ValueError("resunit: no fp32x6 split pack")
+    if out is None:
+        out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)
+    a = _ffi.ResunitArgs()
+    a.dtype = dtype_id(x.dtype)
+    a.x, a.n, a.h, a.w, a.c, a.ldx = x.ptr, x.B, x.H, x.W, x.c, x.ld
+    a.y, a.ldy = out.ptr, out.ld
+    a.w1s, a.w2s, a.w3s = _dp(ws[0]), _dp(ws[1]), _dp(ws[2])
+    a.b1, a.b2, a.b3 = _dp(p1.bias), _dp(p2.bias), _dp(p3.bias)
+    a.mfma_mode = 2
+    check(_lib().lic_resunit_fwd(ctypes.byref(a), stream_handle()))
+    return out
+
+
 def conv_transpose(x: Act, packs: Sequence[ConvPack], Ho: int, Wo: int, out: Optional[Act] = None, **kw) -> Act:
     if out is None:
         out = Act.empty(x.B, Ho, Wo, packs[0].co, x.dtype, x.t.device)

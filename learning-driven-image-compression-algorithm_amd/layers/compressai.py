@@ -10,6 +10,7 @@ import torch
 import torch.nn as nn
 
 from .._ffi import ACT_LRELU, ACT_RELU, EPI_GATE, EPI_RES_ACT
+from .. import functional as Fn
 from ..functional import Act
 from ._conv import Conv2d
 from .gdn import GDN
@@ -85,6 +86,11 @@ class _ResidualUnit(nn.Module):
         self.relu = nn.ReLU(inplace=True)
 
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        if x.dtype == torch.float32 and Fn.split_mode() == 2:
+            # fp32x6: the whole unit in one launch, intermediates in LDS (csrc/resunit_split.hip)
+            packs = [self.conv[i].packed(x.dtype) for i in (0, 2, 4)]
+            if Fn.resunit_fusable(x, *packs, out=out):
+                return Fn.resunit(x, *packs, out=out)
         t = self.conv[0].run(x, act=ACT_RELU)
         t = self.conv[2].run(t, act=ACT_RELU)
         # out = relu(conv(t) + identity): residual added before the activation
