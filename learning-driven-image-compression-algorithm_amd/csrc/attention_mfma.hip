@@ -38,7 +38,7 @@ template <typename T, int NW, int SPLIT = 0>
 __global__ __launch_bounds__(NW * 64) void win_attn_mfma_kernel(const lic_attn_args a) {
   static_assert(!SPLIT || sizeof(T) == 4, "split products are for fp32 data");
   using SM = SplitMode<2>;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int lr = lane & 31, lh = lane >> 5;
   const int d = a.c / a.heads;
   constexpr int ws = 8;

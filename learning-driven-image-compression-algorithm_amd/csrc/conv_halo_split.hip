@@ -59,7 +59,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_split_kernel(const lic
   int* rowpix = (int*)(smem + p.rp_off);
   float* sbias = (float*)(rowpix + BM);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar wave offsets (no waterfall loops)
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31, lhalf = lane >> 5;
 

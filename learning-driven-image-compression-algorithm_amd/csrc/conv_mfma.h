@@ -39,7 +39,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_mfma_kernel(const lic_conv_
   int8_t* tdy = (int8_t*)(sbias + BN);
   int8_t* tdx = tdy + LIC_MAX_TAPS;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar wave offsets (no waterfall loops)
   const int wm = wave / WN, wn = wave % WN;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;

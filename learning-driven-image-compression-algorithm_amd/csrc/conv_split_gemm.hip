@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256, G1_WPS) void conv1x1_split_kernel(const lic_co
   __shared__ float sbias_s[WTN];
   __shared__ float ct_s[4][32 * 33];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar wave offsets (no waterfall loops)
   const int lrow = lane & 31, lhalf = lane >> 5;
   const int m0 = (blockIdx.x * 4 + wave) * WTM;
   const int n0 = blockIdx.y * WTN;

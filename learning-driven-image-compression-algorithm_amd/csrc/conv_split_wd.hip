@@ -59,7 +59,15 @@ struct WdPlan {
 // VT > 0: a 1x1 convolution whose NTAPS = VT "virtual taps" are VT consecutive 16-channel chunks
 // staged together (one barrier per VT chunks; the halo is the tile itself, VT blocks of BM pixels).
 // Occupancy: two waves per SIMD, four for the one-tile-per-wave small-map configurations (TM = TN = 1).
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0>
+// GEO 1: a plain 3x3 stride-1 launch (taps (dy, dx) = unit 3x3 grid, halo (TH+2) x (TW+2), ci a multiple
+// of 16, TW = 16).  Its addressing is compile-time: the halo's LDS swizzle flips the 16-B half by halo ROW
+// parity (conflict-free for 16-wide tiles: a wave's 32 rows are two tile rows, and ds_read_b128's lane
+// groups then take complementary halves), so a tap's A-fragment address is a per-lane base chosen by
+// the tap row's parity (compile-time) plus a compile-time immediate, and every halo quad's global and
+// LDS offsets are computed once per workgroup (the chunk advances a scalar offset): the per-read
+// address VALU of the general path (~5 per ds_read, half of the kernel's vector instructions,
+// profiles/r03/wd_ablation_pmc.txt) is gone.
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0>
 __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32) ? 4 : 2) void conv_split_wd_kernel(
     const lic_conv_args a, const WdPlan p) {
   using SM = SplitMode<MODE>;
@@ -85,12 +93,18 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   // LDS plane geometry is compile-time (every quad's pixel has a slot): the part offsets fold into
   // the ds_read / ds_write immediate offsets
   constexpr int PLANE = NQ * (NT / 4) * 32, SET = NPA * PLANE;
+  constexpr bool FIX = GEO == 1;
+  // FIX: LDS row stride of the halo in pixel slots; 8-wide tiles pad the 10-px rows to 12 so that the
+  // four tile rows a wave's 32 lanes span land on complementary bank halves (row parity swizzle)
+  constexpr int RS = TW == 8 ? 12 : TW + 2;
+  static_assert(!FIX || (NTAPS == 9 && VT == 0 && (TW == 16 || TW == 8)), "GEO 1: 3x3 stride 1, 8- or 16-wide tiles");
+  static_assert(!FIX || (TH + 2) * RS <= NQ * (NT / 4), "GEO 1: halo slots");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* rowpix = (int*)(smem + p.rp_off);
   float* sbias = (float*)(rowpix + BM);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar wave offsets (no waterfall loops)
   const int wm = wave / WN, wn = wave % WN;
   const int lrow = lane & 31, lhalf = lane >> 5;
 
@@ -161,7 +175,25 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   const __amdgpu_buffer_rsrc_t xrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)xg, (short)0, (int)((int64_t)a.n * a.h * a.w * a.ldx * 4), 0x00020000);
   u32x4 hreg[NQ];
+  // FIX: per-quad byte offsets, once per workgroup (global: -> 0x80000000 = reads zeros; LDS: row-parity swizzle)
+  unsigned qv[FIX ? NQ : 1];
+  int ql[FIX ? NQ : 1];
+  if constexpr (FIX) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int hp = (tid >> 2) + i * (NT / 4);   // LDS slot
+      const int r = hp / RS, cc = hp - r * RS;
+      const int iy = iy0 + r, ix = ix0 + cc;
+      const bool ok = r < TH + 2 && cc < TW + 2 && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+      qv[i] = ok ? (unsigned)((((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4) * 4) : 0x80000000u;
+      ql[i] = hp * 32 + (((c4 >> 1) ^ (r & 1)) << 4) + (c4 & 1) * 8;
+    }
+  }
   auto load_quad = [&](int i, int k) {
+    if constexpr (FIX) {
+      hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, qv[i], k * CSTEP * 4, WD_HALO_AUX);
+      return;
+    }
     int cq;
     const int q = quad_off(i, cq);
     const unsigned off = (q >= 0 && k * CSTEP + cq < a.ci) ? (unsigned)(q + k * CSTEP) * 4u : 0x80000000u;
@@ -174,8 +206,8 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
     uint2 parts[NPA];
     const u32x4 h = hreg[i];
     split4<MODE>(make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w)),
-                 pro, sg, parts);
-    const int off = hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
+                 FIX ? (int)LIC_PRO_NONE : pro, sg, parts);
+    const int off = FIX ? ql[i] : hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
 #pragma unroll
     for (int pl = 0; pl < NPA; ++pl) *(uint2*)(set + pl * PLANE + off) = parts[pl];
   };
@@ -190,8 +222,26 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   // per-chunk opaque copy of hbase: the per-tap fragment addresses are then computed in the chunk,
   // not hoisted out of the chunk loop as NTAPS x TM live registers (which spilled)
   int hb[TM];
-  // part pl of the A fragments of the tap at halo offset `toff` (scalar tap cursor, see chunk)
+  // FIX: per-lane A bases by tap-row parity s (lane's halo pixel of tap (0,0), half lhalf ^ row parity)
+  int abase[FIX ? 2 : 1][TM], ab[FIX ? 2 : 1][TM];
+  if constexpr (FIX) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mm = wm * WTM + i * 32 + lrow, ty = mm / TW, tx = mm % TW;
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) abase[sp][i] = (ty * RS + tx) * 32 + ((lhalf ^ ((ty + sp) & 1)) << 4);
+    }
+  }
+  // part pl of the A fragments of the tap at halo offset `toff` (scalar tap cursor, see chunk);
+  // FIX: `toff` is the compile-time tap index
   auto load_a_part = [&](const char* set, int toff, int pl, u32x4(&fa)[NPA][TM]) {
+    if constexpr (FIX) {
+      const int ty = toff / 3, tx = toff - ty * 3;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[pl][i] = *(const u32x4*)(smem + ab[ty & 1][i] + ((ty * RS + tx) * 32 + pl * PLANE));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int hp = hb[i] + toff;
@@ -287,11 +337,18 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = -acc[i][j];
 #endif
-    int toff = p.toff0, cx = 0;   // tap grid cursor (scalar)
+    int toff = FIX ? 0 : p.toff0, cx = 0;   // tap grid cursor (scalar; FIX: the tap index)
+    if constexpr (FIX) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      hb[i] = hbase[i];
-      asm volatile("" : "+v"(hb[i]));
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) ab[sp][i] = abase[sp][i] + (k & 1) * SET;
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        hb[i] = hbase[i];
+        asm volatile("" : "+v"(hb[i]));
+      }
     }
 #pragma unroll
     for (int pl = 0; pl < NPA; ++pl) load_a_part(set, toff, pl, fa);
@@ -303,7 +360,9 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
 #if !(WD_ABL & 2)
       load_b(k * NTAPS + t + PD, fb[(sr + PD) % R]);
 #endif
-      if (t + 1 < NTAPS) {
+      if constexpr (FIX) {
+        toff = t + 1;
+      } else if (t + 1 < NTAPS) {
         toff += p.xstep;
         if (++cx == p.nx) {
           cx = 0;
@@ -370,7 +429,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   }
 }
 
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0>
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0>
 static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   constexpr int NT = WM * WN * 64;
   constexpr int NPA = SplitMode<MODE>::NPA;
@@ -421,6 +480,14 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
     p.xstep = TH * TW;
     p.ystep = 0;
   }
+  static const bool geo_on = [] {
+    const char* e = getenv("LIC_WD_GEO");
+    return !(e && e[0] == '0');
+  }();
+  if (GEO == 1 && (!geo_on || !(a.ntaps == 9 && nx == 3 && p.xstep == 1 && p.ystep == p.hw && p.hw == TW + 2 && p.hsy == 1 &&
+                    p.hsx == 1 && p.toff0 == 0 && a.isy == 1 && a.isx == 1 && a.ci % 16 == 0 &&
+                                  a.prologue == LIC_PRO_NONE)))
+    return 0;
   p.tiles_y = (a.mi + TH - 1) / TH;
   p.tiles_x = (a.mj + TW - 1) / TW;
   p.nchunks = a.cpad / (16 * (VT > 0 ? VT : 1));
@@ -444,7 +511,7 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   }();
   p.ncb = (remap_on && ncb > 1 && blocks % 8 == 0) ? ncb : 0;
   dim3 grid = p.ncb ? dim3((unsigned)(blocks * ncb), 1) : dim3((unsigned)blocks, ncb);
-  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT>;
+  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT, GEO>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
     status = fail(std::string("split wd conv: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -475,15 +542,23 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   // two waves, one 32x32 accumulator each
   if (a.copad == 32 && a.mi >= 8 && a.mj >= 8) {
     if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2>(a, s, status);
-    if (a.ntaps == 9) return try_split_wd<2, 9, 8, 8, 32, 2, 1, 4>(a, s, status);
+    if (a.ntaps == 9) {
+      if (try_split_wd<2, 9, 8, 8, 32, 2, 1, 4, 0, 1>(a, s, status)) return 1;
+      return try_split_wd<2, 9, 8, 8, 32, 2, 1, 4>(a, s, status);
+    }
   }
   if (a.mi >= 8 && a.mj >= 8 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8) && blocks(8, 8, 64) >= 64) {
     if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
-    if (a.ntaps == 9) return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);
+    if (a.ntaps == 9) {
+      if (try_split_wd<2, 9, 8, 8, 64, 2, 2, 2, 0, 1>(a, s, status)) return 1;
+      return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);
+    }
   }
   if (a.mi > 8 && a.mj > 8 && blocks(16, 16, 64) >= 256) {
     switch (a.ntaps) {
-      case 9: return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3, ConvT phase 3x3
+      case 9:   // plain 3x3 stride 1: compile-time addressing (GEO 1); other 3x3 grids (ConvT phases) general
+        if (try_split_wd<2, 9, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status)) return 1;
+        return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);
       case 6: return try_split_wd<2, 6, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phases 3x2 / 2x3
       case 4: return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phase 2x2, 3x3 s2 phase
       case 2: return try_split_wd<2, 2, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3 s2 phases 2x1 / 1x2

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256, 1) void resunit_split_kernel(const lic_resunit
   char* const t1s = smem + 3 * XPL;
   char* const t2s = smem;   // after GEMM1 (a barrier separates the last x read from the first t2 write)
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar wave offsets (no waterfall loops)
   const int lrow = lane & 31, lhalf = lane >> 5;
   const int tiles_x = a.w >> 3, tiles_y = a.h >> 3;
   int bid = blockIdx.x;

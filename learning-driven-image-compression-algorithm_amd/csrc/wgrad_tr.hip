@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_tr_kernel(const lic_wgrad_args a
   constexpr int ZU = ZPIX * 8 / 256, XU = (HPIX * XCH + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar wave offsets (no waterfall loops)
   const int wm = wave >> 1, wn = wave & 1;
   int bx = blockIdx.x;
   const int grp = bx % p.ngroups;
