@@ -11,7 +11,7 @@ s_model, syntax head, metrics).  Prints ONE JSON line on rank 0.
 The headline runs at fp32 grade (the reference computes in fp32, model/net_ga.py:981-1144):
 `--precision auto` (default) times precision='fp32x6' -- fp32 activations and accumulation, every
 conv product formed from six bf16 MFMA products of exact three-part splits (all 24 significand
-bits, fp32 exponent range, dropped terms <= 2^-26 relative; csrc/conv_halo_split.hip) -- when
+bits, fp32 exponent range, dropped terms <= 2^-26 relative; csrc/conv_split_wd.hip) -- when
 its parity leg on the TIMED batch (seed-0 weights, seed-1000 input of rank 0) meets the
 north-star bar with no more flipped symbols (oracle near-ties and their cascades) than the
 exact-fp32 path on the same batch, else exact fp32 (v_mfma_f32_32x32x2_f32).  Extra
@@ -101,10 +101,28 @@ def capture(fn, warm=2):
             fn()
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
+    try:
+        g = torch.cuda.CUDAGraph(keep_graph=True)   # keeps the hipGraph for graph_nodes()
+    except TypeError:
+        g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         out = fn()
     return g, out
+
+
+def graph_nodes(g):
+    """Nodes (kernel launches, memsets, copies) of one captured step: hipGraphGetNodes on the
+    raw graph torch keeps (None when this torch build does not expose it)."""
+    import ctypes
+    try:
+        raw = g.raw_cuda_graph()
+        hip = ctypes.CDLL("libamdhip64.so")
+        n = ctypes.c_size_t(0)
+        if hip.hipGraphGetNodes(ctypes.c_void_p(int(raw)), None, ctypes.byref(n)) != 0:
+            return None
+        return int(n.value)
+    except Exception:
+        return None
 
 
 def time_graph(g, iters):
@@ -398,6 +416,7 @@ def main():
                         "tflops": round(a_tflops, 2), "frac_of_peak": round(a_tflops / peak, 4),
                         "gflop_per_image": gf_a},
             "full_forward_tflops": round(FULL_GFLOP_256 * (args.size / 256) ** 2 * value / world / 1e3, 2),
+            "graph_nodes_per_step": None if args.no_graph else graph_nodes(graph),
         }
         if world == 1 and not args.no_extras:
             result["cpu_baseline"] = cpu_baseline(args.arch, args.size)

@@ -59,8 +59,8 @@ struct WdPlan {
 // VT > 0: a 1x1 convolution whose NTAPS = VT "virtual taps" are VT consecutive 16-channel chunks
 // staged together (one barrier per VT chunks; the halo is the tile itself, VT blocks of BM pixels).
 // Occupancy: two waves per SIMD, four for the one-tile-per-wave small-map configurations (TM = TN = 1).
-// GEO 1: a plain 3x3 stride-1 launch (taps (dy, dx) = unit 3x3 grid, halo (TH+2) x (TW+2), ci a multiple
-// of 16, TW = 16).  Its addressing is compile-time: the halo's LDS swizzle flips the 16-B half by halo ROW
+// GEO 1: a plain K x K stride-1 launch (K = 3 or 7: taps (dy, dx) = unit K x K grid, halo (TH+K-1) x
+// (TW+K-1), ci a multiple of 16, no prologue), or a virtual-tap 1x1 (VT > 0, ci a multiple of the chunk).  Its addressing is compile-time: the halo's LDS swizzle flips the 16-B half by halo ROW
 // parity (conflict-free for 16-wide tiles: a wave's 32 rows are two tile rows, and ds_read_b128's lane
 // groups then take complementary halves), so a tap's A-fragment address is a per-lane base chosen by
 // the tap row's parity (compile-time) plus a compile-time immediate, and every halo quad's global and
@@ -96,9 +96,13 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   constexpr bool FIX = GEO == 1;
   // FIX: LDS row stride of the halo in pixel slots; 8-wide tiles pad the 10-px rows to 12 so that the
   // four tile rows a wave's 32 lanes span land on complementary bank halves (row parity swizzle)
-  constexpr int RS = TW == 8 ? 12 : TW + 2;
-  static_assert(!FIX || (NTAPS == 9 && VT == 0 && (TW == 16 || TW == 8)), "GEO 1: 3x3 stride 1, 8- or 16-wide tiles");
-  static_assert(!FIX || (TH + 2) * RS <= NQ * (NT / 4), "GEO 1: halo slots");
+  // (16-wide tiles: any row stride; a row's 16 lanes cover 8 consecutive columns -> all 8 bank groups)
+  constexpr int KK = NTAPS == 49 ? 7 : 3;
+  constexpr bool FIXK = FIX && VT == 0;   // K x K grid; FIX && VT > 0: virtual-tap 1x1
+  constexpr int RS = TW == 8 ? 12 : TW + KK - 1;
+  static_assert(!FIXK || ((NTAPS == 9 && (TW == 16 || TW == 8)) || (NTAPS == 49 && TW == 16)),
+                "GEO 1: 3x3 on 8- or 16-wide tiles, 7x7 on 16-wide tiles");
+  static_assert(!FIXK || (TH + KK - 1) * RS <= NQ * (NT / 4), "GEO 1: halo slots");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* rowpix = (int*)(smem + p.rp_off);
@@ -182,11 +186,19 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
       const int hp = (tid >> 2) + i * (NT / 4);   // LDS slot
-      const int r = hp / RS, cc = hp - r * RS;
-      const int iy = iy0 + r, ix = ix0 + cc;
-      const bool ok = r < TH + 2 && cc < TW + 2 && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-      qv[i] = ok ? (unsigned)((((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4) * 4) : 0x80000000u;
-      ql[i] = hp * 32 + (((c4 >> 1) ^ (r & 1)) << 4) + (c4 & 1) * 8;
+      if constexpr (FIXK) {
+        const int r = hp / RS, cc = hp - r * RS;
+        const int iy = iy0 + r, ix = ix0 + cc;
+        const bool ok = r < TH + KK - 1 && cc < TW + KK - 1 && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+        qv[i] = ok ? (unsigned)((((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4) * 4) : 0x80000000u;
+        ql[i] = hp * 32 + (((c4 >> 1) ^ (r & 1)) << 4) + (c4 & 1) * 8;
+      } else {   // virtual taps: block `sub` of BM tile pixels carries channels 16 sub .. of the chunk
+        const int sub = hp / BM, m = hp - sub * BM;
+        const int iy = iy0 + (m / TW) * a.isy, ix = ix0 + (m % TW) * a.isx;
+        const bool ok = hp < p.hpix && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+        qv[i] = ok ? (unsigned)((((b * a.h + iy) * a.w + ix) * a.ldx + sub * 16 + c4 * 4) * 4) : 0x80000000u;
+        ql[i] = hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
+      }
     }
   }
   auto load_quad = [&](int i, int k) {
@@ -206,7 +218,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
     uint2 parts[NPA];
     const u32x4 h = hreg[i];
     split4<MODE>(make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(h.z), __uint_as_float(h.w)),
-                 FIX ? (int)LIC_PRO_NONE : pro, sg, parts);
+                 FIXK ? (int)LIC_PRO_NONE : pro, sg, parts);
     const int off = FIX ? ql[i] : hp * 32 + (((c4 >> 1) ^ ((hp >> 3) & 1)) << 4) + (c4 & 1) * 8;
 #pragma unroll
     for (int pl = 0; pl < NPA; ++pl) *(uint2*)(set + pl * PLANE + off) = parts[pl];
@@ -228,18 +240,26 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mm = wm * WTM + i * 32 + lrow, ty = mm / TW, tx = mm % TW;
+      if constexpr (FIXK) {
 #pragma unroll
-      for (int sp = 0; sp < 2; ++sp) abase[sp][i] = (ty * RS + tx) * 32 + ((lhalf ^ ((ty + sp) & 1)) << 4);
+        for (int sp = 0; sp < 2; ++sp) abase[sp][i] = (ty * RS + tx) * 32 + ((lhalf ^ ((ty + sp) & 1)) << 4);
+      } else {   // virtual tap t at slot t * BM + mm: the bit-3 swizzle of mm (BM is a multiple of 16)
+        abase[0][i] = abase[1][i] = mm * 32 + ((lhalf ^ ((mm >> 3) & 1)) << 4);
+      }
     }
   }
   // part pl of the A fragments of the tap at halo offset `toff` (scalar tap cursor, see chunk);
   // FIX: `toff` is the compile-time tap index
   auto load_a_part = [&](const char* set, int toff, int pl, u32x4(&fa)[NPA][TM]) {
-    if constexpr (FIX) {
-      const int ty = toff / 3, tx = toff - ty * 3;
+    if constexpr (FIXK) {
+      const int ty = toff / KK, tx = toff - ty * KK;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
         fa[pl][i] = *(const u32x4*)(smem + ab[ty & 1][i] + ((ty * RS + tx) * 32 + pl * PLANE));
+      return;
+    } else if constexpr (FIX) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[pl][i] = *(const u32x4*)(smem + ab[0][i] + (toff * BM * 32 + pl * PLANE));
       return;
     }
 #pragma unroll
@@ -484,10 +504,14 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
     const char* e = getenv("LIC_WD_GEO");
     return !(e && e[0] == '0');
   }();
-  if (GEO == 1 && (!geo_on || !(a.ntaps == 9 && nx == 3 && p.xstep == 1 && p.ystep == p.hw && p.hw == TW + 2 && p.hsy == 1 &&
-                    p.hsx == 1 && p.toff0 == 0 && a.isy == 1 && a.isx == 1 && a.ci % 16 == 0 &&
-                                  a.prologue == LIC_PRO_NONE)))
-    return 0;
+  if (GEO == 1 && VT == 0) {
+    constexpr int K = NTAPS == 49 ? 7 : 3;
+    if (!geo_on || !(a.ntaps == K * K && nx == K && p.xstep == 1 && p.ystep == p.hw && p.hw == TW + K - 1 &&
+                     p.hsy == 1 && p.hsx == 1 && p.toff0 == 0 && a.isy == 1 && a.isx == 1 && a.ci % 16 == 0 &&
+                     a.prologue == LIC_PRO_NONE))
+      return 0;
+  }
+  if (GEO == 1 && VT > 0 && (!geo_on || a.ci % (16 * VT) != 0)) return 0;
   p.tiles_y = (a.mi + TH - 1) / TH;
   p.tiles_x = (a.mj + TW - 1) / TW;
   p.nchunks = a.cpad / (16 * (VT > 0 ? VT : 1));
@@ -535,24 +559,32 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   // 1x1 (qkv / proj Linear, GDN x^2, skips): 8x16 px x 192 channels, two 16-channel chunks per
   // barrier -- the split of an activation is shared by all 192 output channels
   if (a.ntaps == 1 && a.mi >= 8 && a.mj >= 16 && (int64_t)a.n * a.mi * a.mj >= 65536 && a.cpad % 32 == 0)
-    return try_split_wd<2, 2, 8, 16, 192, 2, 2, 4, 2>(a, s, status);
+    return try_split_wd<2, 2, 8, 16, 192, 2, 2, 4, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 16, 192, 2, 2, 4, 2>(a, s, status);
   // the 16x16 latents of the slice loop / hyper nets (B x 256 px): 8x8 px x 64 channel tiles, one
   // 32x32 accumulator per wave, four waves per SIMD -- the grid is what limits these launches
   // 32 output channels (the slice loop's per-slice mean / scale heads): 8x8 px x 32 channel tiles of
   // two waves, one 32x32 accumulator each
   if (a.copad == 32 && a.mi >= 8 && a.mj >= 8) {
-    if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2>(a, s, status);
+    if (a.ntaps == 1 && a.cpad % 32 == 0)
+      return try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2>(a, s, status);
     if (a.ntaps == 9) {
       if (try_split_wd<2, 9, 8, 8, 32, 2, 1, 4, 0, 1>(a, s, status)) return 1;
       return try_split_wd<2, 9, 8, 8, 32, 2, 1, 4>(a, s, status);
     }
   }
   if (a.mi >= 8 && a.mj >= 8 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8) && blocks(8, 8, 64) >= 64) {
-    if (a.ntaps == 1 && a.cpad % 32 == 0) return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
+    if (a.ntaps == 1 && a.cpad % 32 == 0)
+      return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
     if (a.ntaps == 9) {
       if (try_split_wd<2, 9, 8, 8, 64, 2, 2, 2, 0, 1>(a, s, status)) return 1;
       return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);
     }
+    // one kernel row of a 7x7 (functional.kxk_row_packs): 8 x 14 halo
+    if (a.ntaps == 7) return try_split_wd<2, 7, 8, 8, 64, 2, 2, 2>(a, s, status);
+    // stride-2 phases (5x5: 9/6/6/4 taps, 3x3: 4/2/2/1) and ConvT phases onto small maps
+    if (a.ntaps == 6) return try_split_wd<2, 6, 8, 8, 64, 2, 2, 2>(a, s, status);
+    if (a.ntaps == 4) return try_split_wd<2, 4, 8, 8, 64, 2, 2, 2>(a, s, status);
+    if (a.ntaps == 2) return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2>(a, s, status);
   }
   if (a.mi > 8 && a.mj > 8 && blocks(16, 16, 64) >= 256) {
     switch (a.ntaps) {
@@ -562,7 +594,8 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
       case 6: return try_split_wd<2, 6, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phases 3x2 / 2x3
       case 4: return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phase 2x2, 3x3 s2 phase
       case 2: return try_split_wd<2, 2, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3 s2 phases 2x1 / 1x2
-      case 49: return try_split_wd<2, 49, 16, 16, 64, 4, 2, 4>(a, s, status);   // 7x7: 8 waves, 22x22 halo
+      case 49:   // 7x7: 8 waves, 22x22 halo
+        return try_split_wd<2, 49, 16, 16, 64, 4, 2, 4, 0, 1>(a, s, status) || try_split_wd<2, 49, 16, 16, 64, 4, 2, 4>(a, s, status);
       default: break;
     }
   }

@@ -374,6 +374,41 @@ def stride2_phase_packs(pk: ConvPack) -> Optional[List[ConvPack]]:
     return packs
 
 
+def kxk_row_packs(pk: ConvPack) -> Optional[List[ConvPack]]:
+    """The kernel rows of a stride-1 7x7 ConvPack as 7 one-row sub-packs (7 taps each, biased only in
+    the first), for fp32x6 on small maps (the 16x16 latents): each row runs on the weights-direct
+    8x8-px tiles with an 8 x 14 halo (a 14 x 14 halo does not fit their registers / LDS), the rows
+    accumulated in fp32 through the epilogue's residual operand like the stride-2 phases.  Cached."""
+    if pk.stride != 1 or pk.phase is not None or pk.groups != 1 or pk.kh != 7 or pk.kw != 7 or len(pk.dy) != 49:
+        return None
+    sub = pk.__dict__.get("_rows")
+    if sub is not None and sub[0] is pk.w and sub[1] == pk.w._version:
+        return sub[2]
+    packs = []
+    for ky in range(7):
+        idx = list(range(7 * ky, 7 * ky + 7))
+        packs.append(ConvPack(w=pk.w[:, idx, :].contiguous(), bias=pk.bias if not packs else None, ci=pk.ci,
+                              co=pk.co, dy=[pk.dy[t] for t in idx], dx=[pk.dx[t] for t in idx],
+                              groups=1, stride=1, pad=pk.pad, kh=pk.kh, kw=pk.kw))
+        packs[-1].__dict__["_s2phase_of"] = pk
+    pk.__dict__["_rows"] = (pk.w, pk.w._version, packs)
+    return packs
+
+
+def _accumulate_subpacks(x: Act, subs: Sequence[ConvPack], out: Optional[Act], act: int, slope: float,
+                         prologue: int, hw) -> Act:
+    """One conv as launches of tap subsets into one fp32 output: the first adds the bias, the later
+    ones add the running output as the epilogue residual, the activation goes on the last as
+    RES_ACT, act(acc + b + r1)."""
+    out = conv(x, subs[0], out, prologue=prologue, out_hw=hw)
+    for k, ph in enumerate(subs[1:]):
+        last = k == len(subs) - 2
+        conv(x, ph, out, r1=out, prologue=prologue, out_hw=hw,
+             act=act if last else _ffi.ACT_NONE, slope=slope,
+             epi=_ffi.EPI_RES_ACT if (last and act != _ffi.ACT_NONE) else _ffi.EPI_PLAIN)
+    return out
+
+
 def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT_NONE, slope: float = 0.01,
          epi: int = _ffi.EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
          y2: Optional[Act] = None, prologue: int = _ffi.PRO_NONE, out_hw=None, shuffle: bool = False,
@@ -381,20 +416,24 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     """Run one ConvPack launch. For convT phases `out` (full map) must be given."""
     if (split_mode() == 2 and x.dtype == torch.float32 and not (force_direct or force_generic or shuffle) and
             epi == _ffi.EPI_PLAIN and r1 is None and g is None and r2 is None and
-            y2 is None and x.B * x.H * x.W >= 65536):
+            y2 is None and x.B * x.H * x.W >= 16384):
         phases = stride2_phase_packs(pk)
         if phases is not None and len(phases) > 1:
             # fp32x6 stride-2 k x k conv as its four input-parity phases, accumulated in fp32 through
             # the epilogue's residual operand (the first phase adds the bias); an activation goes on
             # the last phase as RES_ACT, act(acc + b + r1): the same fp32 sum, then the activation
             hw = out_hw if out_hw is not None else conv_out_hw(x.H, x.W, pk)
-            out = conv(x, phases[0], out, prologue=prologue, out_hw=hw)
-            for k, ph in enumerate(phases[1:]):
-                last = k == len(phases) - 2
-                conv(x, ph, out, r1=out, prologue=prologue, out_hw=hw,
-                     act=act if last else _ffi.ACT_NONE, slope=slope,
-                     epi=_ffi.EPI_RES_ACT if (last and act != _ffi.ACT_NONE) else _ffi.EPI_PLAIN)
-            return out
+            return _accumulate_subpacks(x, phases, out, act, slope, prologue, hw)
+    if (split_mode() == 2 and x.dtype == torch.float32 and not (force_direct or force_generic or shuffle) and
+            epi == _ffi.EPI_PLAIN and r1 is None and g is None and r2 is None and y2 is None and pk.kh == 7):
+        hw = out_hw if out_hw is not None else conv_out_hw(x.H, x.W, pk)
+        # the weights-direct 16x16-px tiles take 7x7 maps with >= 256 (tile, 64-channel block) pairs;
+        # smaller maps (the 16x16 latents) run kernel row by kernel row on its 8x8-px tiles
+        t16 = x.B * -(-hw[0] // 16) * -(-hw[1] // 16) * (pk.copad // 64)
+        rows = kxk_row_packs(pk) if (t16 < 256 and min(hw) >= 8 and x.B * (hw[0] // 8) * (hw[1] // 8) *
+                                     (pk.copad // 64) >= 64 and pk.ci % 16 == 0) else None
+        if rows is not None:
+            return _accumulate_subpacks(x, rows, out, act, slope, prologue, hw)
     if x.c != pk.ci:
         raise ValueError(f"conv: input has {x.c} channels, weights expect {pk.ci}")
     if pk.w.dtype != x.dtype:

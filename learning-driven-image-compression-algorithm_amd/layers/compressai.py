@@ -4,6 +4,7 @@ with compressai's parameter names, executed on liblic.
 
 Call sites: layers/layers.py:14-21,87-102; model/net_ga.py:52-59,153,271,295,746,857.
 """
+import os
 from typing import Optional
 
 import torch
@@ -78,6 +79,9 @@ class ResidualBlockWithStride(nn.Module):
         return self.run(Act.from_nchw(x)).nchw()
 
 
+_FUSED_RU = os.environ.get("LIC_FUSED_RU", "1") != "0"   # A/B switch for the fused fp32x6 unit
+
+
 class _ResidualUnit(nn.Module):
     def __init__(self, N):
         super().__init__()
@@ -86,7 +90,7 @@ class _ResidualUnit(nn.Module):
         self.relu = nn.ReLU(inplace=True)
 
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
-        if x.dtype == torch.float32 and Fn.split_mode() == 2:
+        if x.dtype == torch.float32 and Fn.split_mode() == 2 and _FUSED_RU:
             # fp32x6: the whole unit in one launch, intermediates in LDS (csrc/resunit_split.hip)
             packs = [self.conv[i].packed(x.dtype) for i in (0, 2, 4)]
             if Fn.resunit_fusable(x, *packs, out=out):

@@ -41,6 +41,9 @@ DEV = "cuda"
     (256, 1152, 3, 1, (1, 1, 1, 1), 32, 8, "plain"),   # h_s 8x8 map: 8x8 px x 64 ch tiles
     (224, 24, 3, 1, (1, 1, 1, 1), 8, 20, "gelu"),      # copad 32 with 8 masked channels, ragged map
     (128, 32, 1, 1, (0, 0, 0, 0), 32, 16, "plain"),    # 32-channel 1x1 on virtual taps
+    (192, 192, 7, 1, (3, 3, 3, 3), 32, 16, "gelu"),    # 7x7 on the 16x16 latent: 7 kernel-row launches (8x8 tiles)
+    (160, 192, 3, 1, (1, 1, 1, 1), 8, 40, "lrelu_r1"), # 3x3 compile-time addressing (GEO 1), ragged 16x16 tiles
+    (192, 192, 5, 2, (1, 1, 2, 2), 32, 32, "gelu"),    # ZeroPad + 5x5 s2 onto 16x16: 9/6/6/4-tap phases, 8x8 tiles
 ])
 def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     if mode == 1 and (cout % 64 or epi == "gdn"):

@@ -22,12 +22,14 @@ SHAPES = [
     ("wnsa7x7@64", 192, 192, 7, 1, (3, 3, 3, 3), 64),
     ("rbws_conv2@128", 192, 192, 3, 1, (1, 1, 1, 1), 128),
     ("conv5x5s2@128", 192, 192, 5, 2, (1, 1, 2, 2), 128),
+    ("conv5x5s2@32", 192, 192, 5, 2, (1, 1, 2, 2), 32),
     ("qkv1x1@64", 192, 576, 1, 1, (0, 0, 0, 0), 64),
     ("rbneck3x3_96@64", 96, 96, 3, 1, (1, 1, 1, 1), 64),
     ("han3x3_64@256", 64, 64, 3, 1, (1, 1, 1, 1), 256),
     # slice loop / hyper shapes on the 16x16 latent
     ("ru3x3_64@16", 64, 64, 3, 1, (1, 1, 1, 1), 16),
     ("wnsa3x3@16", 192, 192, 3, 1, (1, 1, 1, 1), 16),
+    ("wnsa7x7@16", 192, 192, 7, 1, (3, 3, 3, 3), 16),
     ("cc3x3_224_128@16", 224, 128, 3, 1, (1, 1, 1, 1), 16),
     ("cc3x3_128_48@16", 128, 48, 3, 1, (1, 1, 1, 1), 16),
     ("cc3x3_336_224@16", 336, 224, 3, 1, (1, 1, 1, 1), 16),
