@@ -212,8 +212,8 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
     hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, WD_HALO_AUX);
   };
   // every quad stores (plane_bytes covers NQ * NT/4 pixels): no per-lane branch around the stores
-  auto split_quad = [&](int i, int k, char* set) {
-    const float sg = (WD_ALT && (k & 1)) ? -1.f : 1.f;
+  // sg: the chunk's sign (odd chunks are split from -x); compile-time where the chunk parity is
+  auto split_quad = [&](int i, float sg, char* set) {
     const int hp = (tid >> 2) + i * (NT / 4);
     uint2 parts[NPA];
     const u32x4 h = hreg[i];
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   for (int i = 0; i < NQ; ++i) load_quad(i, 0);
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
-    split_quad(i, 0, smem);
+    split_quad(i, 1.f, smem);
     load_quad(i, 1 < nchunks ? 1 : 0);
   }
 #pragma unroll
@@ -345,10 +345,16 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   // ended chunk k-1 -- and refills those registers with chunk k+2: the split's VALU work and its LDS
   // stores sit between this wave's MFMAs instead of in a serial phase before the barrier.
   constexpr int QPS = (NQ + NTAPS - 1) / NTAPS;
-  auto chunk = [&](int k, auto ks) {
+  // PAR: chunks unrolled in pairs so that a chunk's parity (its plane set, the next chunk's sign) is
+  // a compile-time constant: the sign folds into the split's instructions, the set into LDS offsets
+  constexpr bool PAR = FIX && KU == 1 && NTAPS <= 9 && TW == 8;   // (16-wide: the pair spills)
+  auto chunk = [&](int k, auto ks, auto kpar) {
     constexpr int KS = decltype(ks)::value;
-    const char* set = smem + (k & 1) * SET;
-    char* nset = smem + ((k + 1) & 1) * SET;
+    constexpr int KP = decltype(kpar)::value;   // k & 1 when >= 0
+    const int kodd = KP >= 0 ? KP : (k & 1);
+    const char* set = smem + kodd * SET;
+    char* nset = smem + (kodd ^ 1) * SET;
+    const float nsg = WD_ALT ? (kodd ? 1.f : -1.f) : 1.f;   // sign of chunk k + 1
     const int kn = k + 2 < nchunks ? k + 2 : nchunks - 1;
 #if WD_ALT
     if (k > 0)   // exact sign flip: the running sum changes sign with the chunk's parts
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp)
 #pragma unroll
-        for (int i = 0; i < TM; ++i) ab[sp][i] = abase[sp][i] + (k & 1) * SET;
+        for (int i = 0; i < TM; ++i) ab[sp][i] = abase[sp][i] + kodd * SET;
     } else {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -394,7 +400,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
 #if !(WD_ABL & 1)
 #pragma unroll
         for (int i = t * QPS; i < (t + 1) * QPS && i < NQ; ++i) {
-          split_quad(i, k + 1, nset);
+          split_quad(i, nsg, nset);
 #if WD_ABL & 32   // diagnostic: always chunk 0 (L2-resident): separates HBM latency from the split work
           load_quad(i, 0);
 #else
@@ -407,13 +413,22 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
     }
     __syncthreads();
   };
-  for (int k = 0; k < nchunks; k += KU) {
-    chunk(k, std::integral_constant<int, 0>{});
-    if constexpr (KU == 3) {
+  using NOPAR = std::integral_constant<int, -1>;
+  if constexpr (PAR) {
+    for (int k = 0; k < nchunks; k += 2) {
+      chunk(k, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
       if (k + 1 >= nchunks) break;
-      chunk(k + 1, std::integral_constant<int, 1>{});
-      if (k + 2 >= nchunks) break;
-      chunk(k + 2, std::integral_constant<int, 2>{});
+      chunk(k + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    }
+  } else {
+    for (int k = 0; k < nchunks; k += KU) {
+      chunk(k, std::integral_constant<int, 0>{}, NOPAR{});
+      if constexpr (KU == 3) {
+        if (k + 1 >= nchunks) break;
+        chunk(k + 1, std::integral_constant<int, 1>{}, NOPAR{});
+        if (k + 2 >= nchunks) break;
+        chunk(k + 2, std::integral_constant<int, 2>{}, NOPAR{});
+      }
     }
   }
 
