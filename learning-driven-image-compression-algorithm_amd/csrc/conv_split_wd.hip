@@ -579,7 +579,9 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   // 32x32 accumulator per wave, four waves per SIMD -- the grid is what limits these launches
   // 32 output channels (the slice loop's per-slice mean / scale heads): 8x8 px x 32 channel tiles of
   // two waves, one 32x32 accumulator each
-  if (a.copad == 32 && a.mi >= 8 && a.mj >= 8) {
+  // (maps down to 4x4 -- the hyper prior's -- take the 8x8 tiles partly masked: latency-bound either way,
+  // and the exact-fp32 MFMA chain they otherwise fall back to is 16x slower per product)
+  if (a.copad == 32 && a.mi >= 4 && a.mj >= 4) {
     if (a.ntaps == 1 && a.cpad % 32 == 0)
       return try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2>(a, s, status);
     if (a.ntaps == 9) {
@@ -587,7 +589,7 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
       return try_split_wd<2, 9, 8, 8, 32, 2, 1, 4>(a, s, status);
     }
   }
-  if (a.mi >= 8 && a.mj >= 8 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8) && blocks(8, 8, 64) >= 64) {
+  if (a.mi >= 4 && a.mj >= 4 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8) && blocks(8, 8, 64) >= 32) {
     if (a.ntaps == 1 && a.cpad % 32 == 0)
       return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
     if (a.ntaps == 9) {

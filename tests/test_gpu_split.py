@@ -44,6 +44,8 @@ DEV = "cuda"
     (192, 192, 7, 1, (3, 3, 3, 3), 32, 16, "gelu"),    # 7x7 on the 16x16 latent: 7 kernel-row launches (8x8 tiles)
     (160, 192, 3, 1, (1, 1, 1, 1), 8, 40, "lrelu_r1"), # 3x3 compile-time addressing (GEO 1), ragged 16x16 tiles
     (192, 192, 5, 2, (1, 1, 2, 2), 32, 32, "gelu"),    # ZeroPad + 5x5 s2 onto 16x16: 9/6/6/4-tap phases, 8x8 tiles
+    (64, 64, 3, 1, (1, 1, 1, 1), 32, 4, "lrelu_r1"),   # 4x4 hyper-prior map: one 8x8 tile, 3/4 masked
+    (128, 32, 3, 1, (1, 1, 1, 1), 32, 4, "plain"),     # 4x4 map, 32-channel tile
 ])
 def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
     if mode == 1 and (cout % 64 or epi == "gdn"):
