@@ -565,6 +565,11 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
 // Returns 1 and launches when a weights-direct tile applies, 0 to let the caller try the
 // LDS-staged split kernel (conv_halo_split.hip) or the exact-fp32 kernels.
 int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
+  // A/B switch (LIC_WD_SMALL1X1=0): 1x1 launches on small maps go to the register GEMM (conv_split_gemm.hip)
+  static const bool small1x1 = [] {
+    const char* e = getenv("LIC_WD_SMALL1X1");
+    return !(e && e[0] == '0');
+  }();
   if (a.mfma_mode != 2 || !a.wgt_split || a.dtype != LIC_F32) return 0;
   if (a.groups != 1 || a.ntaps < 1 || a.force_direct || a.force_mfma_generic) return 0;
   if (a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE && a.prologue != LIC_PRO_ABS) return 0;
@@ -582,7 +587,7 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   // (maps down to 4x4 -- the hyper prior's -- take the 8x8 tiles partly masked: latency-bound either way,
   // and the exact-fp32 MFMA chain they otherwise fall back to is 16x slower per product)
   if (a.copad == 32 && a.mi >= 4 && a.mj >= 4) {
-    if (a.ntaps == 1 && a.cpad % 32 == 0)
+    if (a.ntaps == 1 && a.cpad % 32 == 0 && small1x1)
       return try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 32, 2, 1, 4, 2>(a, s, status);
     if (a.ntaps == 9) {
       if (try_split_wd<2, 9, 8, 8, 32, 2, 1, 4, 0, 1>(a, s, status)) return 1;
@@ -590,7 +595,7 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
     }
   }
   if (a.mi >= 4 && a.mj >= 4 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8) && blocks(8, 8, 64) >= 32) {
-    if (a.ntaps == 1 && a.cpad % 32 == 0)
+    if (a.ntaps == 1 && a.cpad % 32 == 0 && small1x1)
       return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
     if (a.ntaps == 9) {
       if (try_split_wd<2, 9, 8, 8, 64, 2, 2, 2, 0, 1>(a, s, status)) return 1;

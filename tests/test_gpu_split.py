@@ -48,8 +48,8 @@ DEV = "cuda"
     (128, 32, 3, 1, (1, 1, 1, 1), 32, 4, "plain"),     # 4x4 map, 32-channel tile
 ])
 def test_split_conv_matches_fp32(cin, cout, k, s, pad, B, H, epi, mode):
-    if mode == 1 and (cout % 64 or epi == "gdn"):
-        pytest.skip("fp32x3 (an extra) keeps the LDS-staged split kernel: 64-channel blocks, no 1x1 GEMM case")
+    if mode == 1 and (cout % 64 or epi == "gdn" or H < 8):
+        pytest.skip("fp32x3 (an extra) keeps the LDS-staged split kernel: 64-channel blocks, maps >= 8, no 1x1 GEMM case")
     import lic_amd.functional as Fn
     from lic_amd import _ffi as L
     from lic_amd.layers import Conv2d
