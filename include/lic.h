@@ -479,6 +479,15 @@ int lic_dwconv_wgrad(int32_t dtype, const void* x, int32_t ldx, const void* dz, 
                      int32_t ntaps, const int8_t* dy, const int8_t* dx, float* dw, float* ws,
                      int64_t ws_bytes, lic_stream_t stream);
 
+/* Patch (im2col) map of a small-channel input for one conv's taps (fp32):
+ *   y[b, i, j, t*c + ch] = x[b, i*stride + dy[t], j*stride + dx[t], ch] (zero outside the map),
+ *   channels [ntaps*c, cpad) zero; dy / dx host arrays, ntaps <= 32.  Lets the image's first conv
+ *   (Cin 3, ResidualBlockWithStride.conv1 at net_ga.py:271) run as a 1x1 conv with K = 27 -> 32 instead
+ *   of 9 taps of a 16-channel-padded input.                                        */
+int lic_patches(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ldx,
+                int32_t ho, int32_t wo, int32_t stride, int32_t ntaps, const int8_t* dy, const int8_t* dx,
+                void* y, int32_t ldy, int32_t cpad, lic_stream_t stream);
+
 /* compressai AttentionBlock ResidualUnit(N) in one launch, fp32 activations with fp32x6 split
  * products (mfma_mode 2):  y = relu(conv1x1_{N/2->N}(relu(conv3x3_{N/2->N/2}(relu(conv1x1_{N->N/2}(x)))))
  * + x), conv3x3 zero-padded by 1.  Replaces the three lic_conv2d_fwd launches of one ResidualUnit

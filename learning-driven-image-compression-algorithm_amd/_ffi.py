@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "lic_layernorm_bwd", "lic_gate_fwd", "lic_half_tanh_fwd", "lic_half_tanh_bwd", "lic_avgpool_bwd",
     "lic_rate_train_parts", "lic_rate_train_fwd", "lic_rate_train_bwd", "lic_recon_train_blocks",
     "lic_recon_train_fwd", "lic_recon_train_bwd", "lic_dwconv_wgrad_workspace", "lic_dwconv_wgrad",
-    "lic_resunit_fwd",
+    "lic_resunit_fwd", "lic_patches",
 )
 LIC_EB_PARAMS = 58
 
@@ -217,6 +217,7 @@ def load():
         "lic_recon_train_bwd": [I, V, I, I, I, I, V, I, V, V, F, V, I, V, V, L, V],
         "lic_dwconv_wgrad": [I, V, I, V, I, I, I, I, I, I, I, I, I, V, V, V, V, L, V],
         "lic_resunit_fwd": [V, V],
+        "lic_patches": [I, V, I, I, I, I, I, I, I, I, I, V, V, V, I, I, V],
     }
     for name, argt in sig.items():
         fn = getattr(lib, name)

@@ -171,3 +171,55 @@ extern "C" int lic_avgpool(int32_t dtype, const void* x, int32_t n, int32_t hw, 
   LIC_CHECK_LAUNCH();
   return 0;
 }
+
+namespace lic {
+
+// Patch (im2col) map of a small-channel input for one conv's taps, fp32:
+//   y[b, i, j, t*c + ch] = x[b, i*s + dy[t], j*s + dx[t], ch]   (zero outside the map),
+//   channels [ntaps*c, cpad) zero.  One thread per output element.
+struct PatchTaps {
+  int8_t dy[32], dx[32];
+};
+
+__global__ void patches_kernel(const float* __restrict__ x, int n, int h, int w, int c, int ldx, int ho, int wo,
+                               int s, int ntaps, PatchTaps tp, float* __restrict__ y, int ldy, int cpad) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)n * ho * wo * cpad;
+  if (idx >= total) return;
+  const int k = (int)(idx % cpad);
+  const int64_t pix = idx / cpad;
+  const int j = (int)(pix % wo);
+  const int64_t q = pix / wo;
+  const int i = (int)(q % ho);
+  const int b = (int)(q / ho);
+  const int t = k / c, ch = k - t * c;
+  float v = 0.f;
+  if (t < ntaps) {
+    const int iy = i * s + tp.dy[t], ix = j * s + tp.dx[t];
+    if ((unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w) v = x[(((int64_t)b * h + iy) * w + ix) * ldx + ch];
+  }
+  y[pix * ldy + k] = v;
+}
+
+}  // namespace lic
+
+extern "C" int lic_patches(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ldx,
+                           int32_t ho, int32_t wo, int32_t stride, int32_t ntaps, const int8_t* dy, const int8_t* dx,
+                           void* y, int32_t ldy, int32_t cpad, lic_stream_t stream) {
+  using namespace lic;
+  if (dtype != LIC_F32) return fail("patches: fp32 only");
+  if (!x || !y || !dy || !dx) return fail("patches: null pointer");
+  if (n < 1 || h < 1 || w < 1 || c < 1 || ho < 1 || wo < 1 || stride < 1 || ntaps < 1 || ntaps > 32)
+    return fail("patches: bad geometry");
+  if (ntaps * c > cpad || ldy < cpad || ldx < c) return fail("patches: ntaps*c must fit cpad <= ldy, c <= ldx");
+  PatchTaps tp{};
+  for (int t = 0; t < ntaps; ++t) {
+    tp.dy[t] = dy[t];
+    tp.dx[t] = dx[t];
+  }
+  const int64_t total = (int64_t)n * ho * wo * cpad;
+  hipLaunchKernelGGL(patches_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)x, n, h, w, c, ldx, ho, wo, stride, ntaps, tp, (float*)y, ldy, cpad);
+  LIC_CHECK_LAUNCH();
+  return 0;
+}

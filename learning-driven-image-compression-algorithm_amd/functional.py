@@ -488,6 +488,36 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     return out
 
 
+def pack_conv2d_patches(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad, c: int,
+                        dtype: torch.dtype):
+    """A k x k conv on a c-channel input (the image, c = 3) as a 1x1 conv over its patch map
+    (lic_patches): weights [copad][1][cpad], channel t*c + ch = w[:, ch, ky, kx] with t = ky*kw + kx,
+    cpad = k*k*c rounded up to 32.  Returns (pack, dy, dx, stride)."""
+    co, cig, kh, kw = weight.shape
+    pt, pl = pad[0], pad[1]
+    K = kh * kw * c
+    cpad = -(-K // 32) * 32
+    copad = _choose_copad(co)
+    w = torch.zeros((copad, 1, cpad), dtype=dtype, device=weight.device)
+    w[:co, 0, :K] = weight.detach()[:, :c].permute(0, 2, 3, 1).reshape(co, K).to(dtype)
+    dy = [ky - pt for ky in range(kh) for kx in range(kw)]
+    dx = [kx - pl for ky in range(kh) for kx in range(kw)]
+    b = bias.detach().float().contiguous() if bias is not None else None
+    return ConvPack(w=w, bias=b, ci=cpad, co=co, dy=[0], dx=[0]), dy, dx, stride
+
+
+def patches(x: Act, dy: Sequence[int], dx: Sequence[int], stride: int, Ho: int, Wo: int, cpad: int) -> Act:
+    """lic_patches: the patch map [B, Ho, Wo, cpad] of x for the taps (dy, dx) at `stride`."""
+    if x.dtype != torch.float32:
+        raise ValueError("patches: fp32 only")
+    out = Act.empty(x.B, Ho, Wo, cpad, x.dtype, x.t.device)
+    nt = len(dy)
+    ady, adx = (ctypes.c_int8 * nt)(*dy), (ctypes.c_int8 * nt)(*dx)
+    check(_lib().lic_patches(_ffi.LIC_F32, x.ptr, x.B, x.H, x.W, x.c, x.ld, Ho, Wo, stride, nt, ady, adx,
+                             out.ptr, out.ld, cpad, stream_handle()))
+    return out
+
+
 _TAPS3 = ([-1, -1, -1, 0, 0, 0, 1, 1, 1], [-1, 0, 1, -1, 0, 1, -1, 0, 1])
 
 

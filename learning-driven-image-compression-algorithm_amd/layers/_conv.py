@@ -7,6 +7,7 @@ Packed weights ([copad][taps][cpad] in the activation dtype) are cached per
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -15,6 +16,9 @@ import torch.nn as nn
 from .. import functional as Fn
 from .._ffi import ACT_NONE, EPI_PLAIN, PRO_NONE
 from ..functional import Act
+
+
+_PATCHES = os.environ.get("LIC_PATCHES", "1") != "0"   # A/B switch for the fp32x6 first-conv patch path
 
 
 def _param_key(*ps):
@@ -46,6 +50,20 @@ class Conv2d(nn.Conv2d, _PackCache):
     def run(self, x: Act, out: Optional[Act] = None, *, pad=None, act: int = ACT_NONE, slope: float = 0.01,
             epi: int = EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
             y2: Optional[Act] = None, prologue: int = PRO_NONE, shuffle: bool = False) -> Act:
+        k = self.kernel_size[0]
+        if (Fn.split_mode() == 2 and x.dtype == torch.float32 and self.groups == 1 and x.c == self.in_channels and
+                x.c <= 4 and 1 < k * k * x.c <= 32 and prologue == PRO_NONE and not shuffle and _PATCHES):
+            # fp32x6, the image's k x k conv (Cin 3): one 1x1 launch over the patch map (K = 27 -> 32)
+            # instead of k*k taps of a 16-channel-padded input on the exact-fp32 kernel
+            if pad is None:
+                p = self.padding[0]
+                pad = (p, p, p, p)
+            pk, dy, dx, s = self._get_pack((x.dtype, pad, "patches", x.c), lambda: Fn.pack_conv2d_patches(
+                self.weight, self.bias, self.stride[0], pad, x.c, x.dtype))
+            Ho, Wo = Fn.conv_out_hw(x.H, x.W, Fn.ConvPack(w=pk.w, bias=None, ci=x.c, co=self.out_channels,
+                                                        dy=dy, dx=dx, stride=s, pad=pad, kh=k, kw=k))
+            pm = Fn.patches(x, dy, dx, s, Ho, Wo, pk.cpad)
+            return Fn.conv(pm, pk, out, act=act, slope=slope, epi=epi, r1=r1, g=g, r2=r2, y2=y2)
         epc = 16 // x.t.element_size()
         if self.groups == 1 and x.c % epc and x.zpad >= -(-x.c // epc) * epc and x.c == self.in_channels:
             # zero-padded small-channel input (e.g. the 3-channel image): run as Cin = 16 B on MFMA

@@ -164,3 +164,31 @@ def test_split_conv_transpose_phases(mode):
     print(f"\n[split{mode} convT5x5 s2 B=32 32^2] max err vs torch {err:.2e}, vs exact kernel {err0:.2e} (scale {scale:.2f})")
     assert not torch.equal(got, exact)
     assert err <= 3e-6 * scale and err0 <= 5e-6 * scale
+
+
+@pytest.mark.parametrize("k,s,act", [(3, 2, "lrelu"), (1, 2, "none"), (3, 1, "none")])
+def test_split_patch_path_first_conv(k, s, act):
+    """fp32x6: a k x k conv on the 3-channel image runs as a 1x1 conv over its patch map
+    (lic_patches, K = 27 -> 32; ResidualBlockWithStride.conv1 / skip at net_ga.py:271)."""
+    import lic_amd.functional as Fn
+    from lic_amd import _ffi as L
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(5 + k + s)
+    m = Conv2d(3, 192, k, s, k // 2).to(DEV)
+    with torch.no_grad():
+        m.bias.normal_(0, 0.1)
+    x = torch.rand(8, 3, 64, 64) * 2 - 1
+    t = torch.zeros(8, 64, 64, 4, device=DEV)
+    t[..., :3] = x.permute(0, 2, 3, 1).to(DEV)
+    X = Fn.Act(t, 0, 3, zpad=4)
+    kw = dict(act=L.ACT_LRELU) if act == "lrelu" else {}
+    exact = m.run(X, **kw).nchw().cpu()
+    with Fn.split_f32(2):
+        got = m.run(X, **kw).nchw().cpu()
+    base = F.conv2d(x.double(), m.weight.detach().cpu().double(), m.bias.detach().cpu().double(), s, k // 2)
+    if act == "lrelu":
+        base = F.leaky_relu(base, 0.01)
+    scale = base.abs().max().item()
+    assert got.shape == exact.shape == base.shape
+    assert (got.double() - base).abs().max().item() <= 3e-6 * scale
+    assert (got - exact).abs().max().item() <= 5e-6 * scale

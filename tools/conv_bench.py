@@ -36,6 +36,8 @@ SHAPES = [
     ("ru1x1_128_64@16", 128, 64, 1, 1, (0, 0, 0, 0), 16),
     ("ru1x1_64_128@16", 64, 128, 1, 1, (0, 0, 0, 0), 16),
     ("lin512_128@16", 512, 128, 1, 1, (0, 0, 0, 0), 16),
+    ("lin128_512@16", 128, 512, 1, 1, (0, 0, 0, 0), 16),
+    ("in1x1_320_128@16", 320, 128, 1, 1, (0, 0, 0, 0), 16),
     ("proj1x1@64", 192, 192, 1, 1, (0, 0, 0, 0), 64),
     ("gdn1x1@128", 192, 192, 1, 1, (0, 0, 0, 0), 128),
     ("cc3x3_128_32@16", 128, 32, 3, 1, (1, 1, 1, 1), 16),
