@@ -167,12 +167,14 @@ def test_split_conv_transpose_phases(mode):
 
 
 @pytest.mark.parametrize("k,s,act", [(3, 2, "lrelu"), (1, 2, "none"), (3, 1, "none")])
-def test_split_patch_path_first_conv(k, s, act):
+def test_split_patch_path_first_conv(k, s, act, monkeypatch):
     """fp32x6: a k x k conv on the 3-channel image runs as a 1x1 conv over its patch map
-    (lic_patches, K = 27 -> 32; ResidualBlockWithStride.conv1 / skip at net_ga.py:271)."""
+    (lic_patches, K = 27 -> 32; ResidualBlockWithStride.conv1 / skip at net_ga.py:271); opt-in path."""
     import lic_amd.functional as Fn
     from lic_amd import _ffi as L
     from lic_amd.layers import Conv2d
+    import lic_amd.layers._conv as C
+    monkeypatch.setattr(C, "_PATCHES", True)
     torch.manual_seed(5 + k + s)
     m = Conv2d(3, 192, k, s, k // 2).to(DEV)
     with torch.no_grad():
@@ -190,5 +192,6 @@ def test_split_patch_path_first_conv(k, s, act):
         base = F.leaky_relu(base, 0.01)
     scale = base.abs().max().item()
     assert got.shape == exact.shape == base.shape
+    assert not torch.equal(got, exact)          # the patch path ran (a different summation order)
     assert (got.double() - base).abs().max().item() <= 3e-6 * scale
     assert (got - exact).abs().max().item() <= 5e-6 * scale
