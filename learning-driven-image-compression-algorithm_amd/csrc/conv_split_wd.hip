@@ -67,7 +67,7 @@ struct WdPlan {
 // LDS offsets are computed once per workgroup (the chunk advances a scalar offset): the per-read
 // address VALU of the general path (~5 per ds_read, half of the kernel's vector instructions,
 // profiles/r03/wd_ablation_pmc.txt) is gone.
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0>
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0>
 __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32) ? 4 : 2) void conv_split_wd_kernel(
     const lic_conv_args a, const WdPlan p) {
   using SM = SplitMode<MODE>;
@@ -97,12 +97,13 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   // FIX: LDS row stride of the halo in pixel slots; 8-wide tiles pad the 10-px rows to 12 so that the
   // four tile rows a wave's 32 lanes span land on complementary bank halves (row parity swizzle)
   // (16-wide tiles: any row stride; a row's 16 lanes cover 8 consecutive columns -> all 8 bank groups)
-  constexpr int KK = NTAPS == 49 ? 7 : 3;
-  constexpr bool FIXK = FIX && VT == 0;   // K x K grid; FIX && VT > 0: virtual-tap 1x1
+  // tap grid KY x KX (KXT > 0: KX = KXT, the rectangular transposed-conv phases; else square)
+  constexpr int KK = KXT > 0 ? KXT : (NTAPS == 49 ? 7 : (NTAPS == 4 ? 2 : 3));
+  constexpr int KY = NTAPS / KK;
+  constexpr bool FIXK = FIX && VT == 0;   // KY x KX grid; FIX && VT > 0: virtual-tap 1x1
   constexpr int RS = TW == 8 ? 12 : TW + KK - 1;
-  static_assert(!FIXK || ((NTAPS == 9 && (TW == 16 || TW == 8)) || (NTAPS == 49 && TW == 16)),
-                "GEO 1: 3x3 on 8- or 16-wide tiles, 7x7 on 16-wide tiles");
-  static_assert(!FIXK || (TH + KK - 1) * RS <= NQ * (NT / 4), "GEO 1: halo slots");
+  static_assert(!FIXK || (KY * KK == NTAPS && (TW == 16 || (TW == 8 && KK <= 3))), "GEO 1: tap grid");
+  static_assert(!FIXK || (TH + KY - 1) * RS <= NQ * (NT / 4), "GEO 1: halo slots");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* rowpix = (int*)(smem + p.rp_off);
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
       if constexpr (FIXK) {
         const int r = hp / RS, cc = hp - r * RS;
         const int iy = iy0 + r, ix = ix0 + cc;
-        const bool ok = r < TH + KK - 1 && cc < TW + KK - 1 && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+        const bool ok = r < TH + KY - 1 && cc < TW + KK - 1 && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
         qv[i] = ok ? (unsigned)((((b * a.h + iy) * a.w + ix) * a.ldx + c4 * 4) * 4) : 0x80000000u;
         ql[i] = hp * 32 + (((c4 >> 1) ^ (r & 1)) << 4) + (c4 & 1) * 8;
       } else {   // virtual taps: block `sub` of BM tile pixels carries channels 16 sub .. of the chunk
@@ -464,7 +465,7 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   }
 }
 
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0>
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0>
 static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   constexpr int NT = WM * WN * 64;
   constexpr int NPA = SplitMode<MODE>::NPA;
@@ -520,8 +521,9 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
     return !(e && e[0] == '0');
   }();
   if (GEO == 1 && VT == 0) {
-    constexpr int K = NTAPS == 49 ? 7 : 3;
-    if (!geo_on || !(a.ntaps == K * K && nx == K && p.xstep == 1 && p.ystep == p.hw && p.hw == TW + K - 1 &&
+    constexpr int K = KXT > 0 ? KXT : (NTAPS == 49 ? 7 : (NTAPS == 4 ? 2 : 3));
+    if (!geo_on || !(a.ntaps == NTAPS && nx == K && p.xstep == (K > 1 ? 1 : 0) && (NTAPS == K || p.ystep == p.hw) &&
+                     p.hw == TW + K - 1 && p.hh == TH + NTAPS / K - 1 &&
                      p.hsy == 1 && p.hsx == 1 && p.toff0 == 0 && a.isy == 1 && a.isx == 1 && a.ci % 16 == 0 &&
                      a.prologue == LIC_PRO_NONE))
       return 0;
@@ -550,7 +552,7 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   }();
   p.ncb = (remap_on && ncb > 1 && blocks % 8 == 0) ? ncb : 0;
   dim3 grid = p.ncb ? dim3((unsigned)(blocks * ncb), 1) : dim3((unsigned)blocks, ncb);
-  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT, GEO>;
+  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT, GEO, KXT>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
     status = fail(std::string("split wd conv: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -613,8 +615,12 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
       case 9:   // plain 3x3 stride 1: compile-time addressing (GEO 1); other 3x3 grids (ConvT phases) general
         if (try_split_wd<2, 9, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status)) return 1;
         return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);
-      case 6: return try_split_wd<2, 6, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phases 3x2 / 2x3
-      case 4: return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);     // ConvT phase 2x2, 3x3 s2 phase
+      case 6:   // ConvT phases 3x2 / 2x3 (compile-time grids when the taps ascend), s2 phases general
+        return try_split_wd<2, 6, 16, 16, 64, 2, 2, 6, 0, 1, 2>(a, s, status) ||
+               try_split_wd<2, 6, 16, 16, 64, 2, 2, 6, 0, 1, 3>(a, s, status) ||
+               try_split_wd<2, 6, 16, 16, 64, 2, 2, 6>(a, s, status);
+      case 4:   // ConvT phase 2x2, 3x3 s2 phase
+        return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status) || try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);
       case 2: return try_split_wd<2, 2, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3 s2 phases 2x1 / 1x2
       case 49:   // 7x7: 8 waves, 22x22 halo
         return try_split_wd<2, 49, 16, 16, 64, 4, 2, 4, 0, 1>(a, s, status) || try_split_wd<2, 49, 16, 16, 64, 4, 2, 4>(a, s, status);

@@ -200,7 +200,9 @@ def pack_conv_transpose2d(weight: torch.Tensor, bias: Optional[torch.Tensor], st
         for rx in range(s):
             kys = [ky for ky in range(kh) if (ry + p - ky) % s == 0]
             kxs = [kx for kx in range(kw) if (rx + p - kx) % s == 0]
-            taps = [(ky, kx) for ky in kys for kx in kxs]
+            # ascending (dy, dx) = descending (ky, kx): a unit-step grid the split kernels address at
+            # compile time (conv_split_wd.hip GEO 1)
+            taps = [(ky, kx) for ky in sorted(kys, reverse=True) for kx in sorted(kxs, reverse=True)]
             if not taps:
                 continue
             cpad = _cpad_for(ci, dtype)
