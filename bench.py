@@ -107,6 +107,13 @@ def capture(fn, warm=2):
         g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         out = fn()
+    # keep_graph=True defers hipGraphInstantiate to the first replay: instantiate (or replay once)
+    # here, so no timed loop pays for it
+    try:
+        g.instantiate()
+    except (AttributeError, RuntimeError):
+        g.replay()
+    torch.cuda.synchronize()
     return g, out
 
 
@@ -222,8 +229,9 @@ def parity_check(arch, precision, size, device, batch=1):
     """The timed batch (rank 0's input, the timed net's seed-0 weights) through the HIP path and
     the CPU oracle: bpp / PSNR deltas, the symbol flips and how many of them are near-ties of the
     oracle's y - mu (|frac - 1/2| < TIE_EPS: fp32 summation order, tests/parity.py), and whether
-    the north-star bar holds (bpp 1e-5, PSNR 1e-4 dB, flips at most 3e-5 of the symbols, each a
-    near-tie or its cascade)."""
+    the north-star bar holds (bpp 1e-5 against the oracle conditioned on the same symbols -- the
+    flips' measured bits reported beside it --, PSNR 1e-4 dB, flips at most 3e-5 of the symbols,
+    each a near-tie or its cascade)."""
     from oracle import ref_cpu as R
     net = build_net(arch, precision, size, batch, "cpu", seed=0)
     P = {k: v.detach().float() for k, v in net.state_dict().items()}
@@ -248,14 +256,28 @@ def parity_check(arch, precision, size, device, batch=1):
                                  for tb, tc, ty, tx in tl))
     d_bpp = abs(bpp.item() - ref["bpp"].item())
     d_psnr = abs(v_psnr.item() - ref["v_psnr"].item())
-    bar = 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (batch * size * size)
+    # rate bar (tests/parity.check_rate): 1e-5 bpp against the oracle on the same symbols -- with
+    # flips, the oracle's slice loop re-run conditioned on this path's symbols; the bits the flips
+    # cost in the oracle's own arithmetic are measured and reported, not budgeted
+    px = batch * size * size
+    bits_free = torch.log2(ref["likelihoods"].double())
+    if flips:
+        sym = net.last["symbols"].cpu()
+        lik_f = R.slice_loop(ref["z3"], ref["latent_means"], ref["latent_scales"], P, forced_symbols=sym)[1]
+        bits_ref = torch.log2(lik_f.double())
+    else:
+        bits_ref = bits_free
+    d_ctx = abs((bits_ref - torch.log2(net.last["likelihoods"].double().cpu())).sum().item()) / px
+    flip_bits = (bits_free - bits_ref).sum().item()
+    bar = 1e-5 * max(1.0, abs(ref["bpp"].item()))
     return {"images": batch, "bpp": round(bpp.item(), 7), "bpp_ref": round(ref["bpp"].item(), 7),
-            "d_bpp": d_bpp, "psnr_db": round(v_psnr.item(), 5), "d_psnr_db": d_psnr,
+            "d_bpp": d_bpp, "d_bpp_same_symbols": d_ctx, "flip_bits": round(flip_bits, 4),
+            "psnr_db": round(v_psnr.item(), 5), "d_psnr_db": d_psnr,
             "symbol_flips": flips, "near_tie_flips": ties, "unexplained_flips": unexplained,
             "symbol_mismatch_frac": flips / ref["symbols"].numel(),
             "batch": f"timed batch of rank 0 (weights seed 0, input seed 1000, {batch} x {size}x{size})",
-            "meets_north_star_bar": bool(d_bpp <= bar and d_psnr <= 1e-4 and flips / ne.numel() <= 3e-5 and
-                                         unexplained == 0)}
+            "meets_north_star_bar": bool(d_ctx <= bar and d_bpp <= bar + abs(flip_bits) / px and d_psnr <= 1e-4
+                                         and flips / ne.numel() <= 3e-5 and unexplained == 0)}
 
 
 def forward_rate(net, x, iters=10):
@@ -300,10 +322,22 @@ def extra_leg(args, other, x, device, gf_a):
                        "error floor 2^-25) and fp16(x) itself below 6.1e-5; reported as an extra")
     elif split == 2:
         leg["note"] = ("fp32 activations and accumulation, each product from six bf16 MFMA products of exact "
-                       "three-part splits (csrc/conv_halo_split.hip, dropped terms <= 2^-26 relative)")
+                       "three-part splits (csrc/conv_split_wd.hip weights-direct kernel for the k x k and 1x1 tiles, "
+                       "conv_split_gemm.hip / conv_halo_split.hip for the rest; dropped terms <= 2^-26 relative)")
     del net2
     torch.cuda.empty_cache()
     return leg
+
+
+def timed_dry(world, k):
+    """The timed region's barrier / clock structure without a GPU (--dry-run)."""
+    from lic_amd import distributed as D
+    D.barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        pass
+    D.barrier(world)
+    return time.perf_counter() - t0
 
 
 def main():
@@ -325,10 +359,27 @@ def main():
     ap.add_argument("--post-processing", action="store_true", help="HAN post-processing head (eval_net flag)")
     ap.add_argument("--profile", action="store_true",
                     help="only warm-up + timed replays (for rocprofv3 per-forward kernel breakdowns)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group check without a GPU: gloo backend, no CUDA call; each rank "
+                         "'processes' its batch as a no-op and rank 0 prints the JSON line's launch fields")
     args = ap.parse_args()
 
     from lic_amd import distributed as D
-    rank, world, local = D.init("nccl")
+    if args.gpus > 1 and not D.launched():
+        # `python bench.py --gpus N` without torchrun: start the N ranks here (one process per GPU,
+        # LOCAL_RANK selects the device), before this process makes any GPU call
+        sys.exit(D.launch_workers([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+    rank, world, local = D.init("gloo" if args.dry_run else "nccl")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    if args.dry_run:
+        elapsed = D.max_over_ranks(timed_dry(world, args.steps), world)
+        if rank == 0:
+            print(json.dumps({"metric": f"images/sec encode+decode ({args.size}x{args.size})", "dry_run": True,
+                              "n_gpus": world, "steps": args.steps, "global_batch": args.batch * world,
+                              "elapsed_s": elapsed, "scaling": "weak"}), flush=True)
+        D.finish(world)
+        return
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     gate = gate32 = None

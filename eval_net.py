@@ -250,7 +250,16 @@ def main(argv=None):
     parser.add_argument("--lambdas", default=",".join(str(v) for v in RD_LAMBDAS),
                         help="comma-separated lambda list for --synthetic-kodak")
     parser.add_argument("--graph", action="store_true", help="hipGraph replay per (lambda, shape)")
+    parser.add_argument("--gpus", type=int, default=1,
+                        help="ranks (one per GPU); without torchrun this process starts them itself")
     args = parser.parse_args(argv)
+    from lic_amd import distributed as D
+    if args.gpus > 1 and not D.launched():
+        # one process per GPU, started before this process touches the GPU (no re-exec)
+        sys.exit(D.launch_workers([sys.executable, os.path.abspath(__file__)] + (sys.argv[1:] if argv is None
+                                                                                 else list(argv)), args.gpus))
+    if D.launched() and D.env_rank()[1] != args.gpus and args.gpus > 1:
+        raise SystemExit(f"eval_net.py: --gpus {args.gpus} but the launcher started {D.env_rank()[1]} ranks")
     if args.synthetic_kodak:
         lambdas = [float(v) for v in args.lambdas.split(",") if v]
         summ, ips, world = rd_sweep(lambdas, args.weight_path, arch=args.arch, precision=args.precision,

@@ -516,7 +516,11 @@ int lic_resunit_fwd(const lic_resunit_args* a, lic_stream_t stream);
 enum { LIC_ARGS_CONV = 0, LIC_ARGS_ATTN = 1, LIC_ARGS_RATE = 2, LIC_ARGS_RANS = 3, LIC_ARGS_WGRAD = 4,
        LIC_ARGS_RESUNIT = 5 };
 const char* lic_last_error(void);
-const char* lic_version(void);
+const char* lic_version(void);          /* "liblic <ver> gfx950 (abi N, src <source hash>)" */
+/* Build provenance: the first 16 hex digits of the SHA-256 of the sources the library was built
+ * from (csrc/ *.hip *.h Makefile in name order, then include/lic.h, concatenated).  The Python host
+ * recomputes it from the tree and refuses a library built from other sources (_ffi.load). */
+const char* lic_source_hash(void);
 int32_t lic_abi_version(void);
 int64_t lic_args_size(int32_t which);   /* sizeof the LIC_ARGS_* struct the library was built with, -1 if unknown */
 int lic_device_arch(char* buf, int32_t len);

@@ -12,6 +12,21 @@ import pathlib
 
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "liblic.so"
+CSRC = _HERE / "csrc"
+HEADER = _HERE.parent / "include" / "lic.h"
+
+
+def source_hash() -> str | None:
+    """csrc/Makefile's SRC_HASH recomputed from the tree: SHA-256 of csrc/ *.hip *.h Makefile in
+    name order, then include/lic.h, first 16 hex digits (None when the sources are not present)."""
+    import hashlib
+    if not CSRC.is_dir() or not HEADER.is_file():
+        return None
+    names = sorted([p.name for p in CSRC.iterdir() if p.is_file() and p.suffix in (".hip", ".h")] + ["Makefile"])
+    h = hashlib.sha256()
+    for p in [CSRC / n for n in names] + [HEADER]:
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
 
 LIC_F32, LIC_F16, LIC_BF16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_GELU, ACT_ROUND = 0, 1, 2, 3, 4
@@ -24,7 +39,8 @@ EXPORTED_SYMBOLS = (
     "lic_conv2d_fwd", "lic_gdn_prepare", "lic_win_attn_fwd", "lic_layernorm_fwd",
     "lic_gauss_rate_fwd", "lic_quantize_median", "lic_bpp_finalize", "lic_syntax_recon_fwd",
     "lic_psnr_finalize", "lic_nchw_to_nhwc", "lic_nhwc_to_nchw", "lic_add", "lic_copy",
-    "lic_avgpool", "lic_rb3_fwd", "lic_last_error", "lic_version", "lic_abi_version", "lic_args_size",
+    "lic_avgpool", "lic_rb3_fwd", "lic_last_error", "lic_version", "lic_source_hash", "lic_abi_version",
+    "lic_args_size",
     "lic_device_arch",
     "lic_gauss_pmf", "lic_eb_pmf", "lic_pmf_to_cdf", "lic_gauss_indexes", "lic_quantize_symbols",
     "lic_rans_cap", "lic_rans_encode", "lic_rans_pack", "lic_rans_decode",
@@ -243,6 +259,12 @@ def load():
     lib.lic_abi_version.restype = ctypes.c_int32
     lib.lic_args_size.argtypes = [I]
     lib.lic_args_size.restype = ctypes.c_int64
+    lib.lic_source_hash.restype = ctypes.c_char_p
+    built, tree = lib.lic_source_hash().decode(), source_hash()
+    if tree is not None and built != tree:
+        _load_error = (f"liblic.so at {path} was built from other sources (hash {built}, this tree {tree}): "
+                       "rebuild it with `make -C learning-driven-image-compression-algorithm_amd/csrc`")
+        raise LicError(_load_error)
     abi = lib.lic_abi_version()
     if abi != ABI_VERSION:
         _load_error = f"liblic ABI {abi} at {path}, this host expects {ABI_VERSION}: rebuild liblic.so"

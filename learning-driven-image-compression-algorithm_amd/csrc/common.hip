@@ -29,7 +29,14 @@ hipError_t ensure_dyn_lds(const void* kern, int bytes) {
 }  // namespace lic
 
 extern "C" const char* lic_last_error(void) { return lic::g_err.c_str(); }
-extern "C" const char* lic_version(void) { return "liblic 0.5 gfx950 (abi 5)"; }
+extern "C" const char* lic_version(void) {
+  static char buf[96];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    snprintf(buf, sizeof(buf), "liblic 0.6 gfx950 (abi %d, src %s)", (int)LIC_ABI_VERSION, lic_source_hash());
+  });
+  return buf;
+}
 extern "C" int32_t lic_abi_version(void) { return LIC_ABI_VERSION; }
 extern "C" int64_t lic_args_size(int32_t which) {
   switch (which) {

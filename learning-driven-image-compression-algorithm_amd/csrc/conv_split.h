@@ -53,9 +53,10 @@ __device__ __forceinline__ void split4(float4 v, int pro, float sg, uint2 (&out)
   if (pro == LIC_PRO_SQUARE) v = make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
   else if (pro == LIC_PRO_ABS) v = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
   float r[4] = {sg * v.x, sg * v.y, sg * v.z, sg * v.w};
-  if constexpr (MODE == 1) {   // fp16 parts: saturate instead of producing inf / NaN (|x| > 65504 is
-#pragma unroll                 // outside fp32x3's domain; the host sends x^2 prologues to mode 2)
-    for (int e = 0; e < 4; ++e) r[e] = fminf(fmaxf(r[e], -65504.f), 65504.f);
+  if constexpr (MODE == 1) {   // fp16 parts: |x| > 65504 is outside fp32x3's domain (the host sends x^2
+#pragma unroll                 // prologues to mode 2); such an input poisons its outputs with NaN, loudly,
+    for (int e = 0; e < 4; ++e)   // instead of a silently saturated finite value
+      r[e] = fabsf(r[e]) <= 65504.f ? r[e] : __builtin_nanf("");
   }
 #pragma unroll
   for (int pl = 0; pl < SplitMode<MODE>::NPA; ++pl) {

@@ -67,8 +67,11 @@ struct WdPlan {
 // LDS offsets are computed once per workgroup (the chunk advances a scalar offset): the per-read
 // address VALU of the general path (~5 per ds_read, half of the kernel's vector instructions,
 // profiles/r03/wd_ablation_pmc.txt) is gone.
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0>
-__global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32) ? 4 : 2) void conv_split_wd_kernel(
+// OCC: waves per SIMD the registers are budgeted for (0: four for the one-tile-per-wave small-map
+// configurations, else two); RF: B-ring slots (0: by the tap count, below)
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0,
+          int OCC = 0, int RF = 0>
+__global__ __launch_bounds__(WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 && BN / WN == 32) ? 4 : 2)) void conv_split_wd_kernel(
     const lic_conv_args a, const WdPlan p) {
   using SM = SplitMode<MODE>;
   using T = typename SM::T;
@@ -82,9 +85,11 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   // 4), so every chunk starts at slot 0; else the chunk loop is unrolled by KU = 3 (chunk k starts
   // at slot (k*NTAPS) % 3)
   // (an even tap count that 3 and 4 do not divide: two slots at prefetch distance one)
-  constexpr int R = (NTAPS % 3 == 0) ? 3 : ((NTAPS % 4 == 0) ? 4 : ((NTAPS % 2 == 0) ? 2 : 3));
+  constexpr int R = RF > 0 ? RF : ((NTAPS % 3 == 0) ? 3 : ((NTAPS % 4 == 0) ? 4 : ((NTAPS % 2 == 0) ? 2 : 3)));
   constexpr int PD = R == 2 ? 1 : 2;   // B prefetch distance in steps
-  constexpr int KU = (NTAPS % R == 0) ? 1 : 3;
+  // chunks per loop trip: the smallest KU with KU * NTAPS a multiple of R
+  constexpr int KU = (NTAPS % R == 0) ? 1 : ((2 * NTAPS) % R == 0 ? 2 : ((3 * NTAPS) % R == 0 ? 3 : 4));
+  static_assert((KU * NTAPS) % R == 0, "B ring");
   constexpr int CSTEP = 16 * (VT > 0 ? VT : 1);   // input channels per chunk
   static_assert(WTM % 32 == 0 && WTN % 32 == 0 && NT % 4 == 0, "tile");
   static_assert(VT == 0 || VT == NTAPS, "virtual taps");
@@ -424,11 +429,17 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   } else {
     for (int k = 0; k < nchunks; k += KU) {
       chunk(k, std::integral_constant<int, 0>{}, NOPAR{});
-      if constexpr (KU == 3) {
+      if constexpr (KU >= 2) {
         if (k + 1 >= nchunks) break;
         chunk(k + 1, std::integral_constant<int, 1>{}, NOPAR{});
+      }
+      if constexpr (KU >= 3) {
         if (k + 2 >= nchunks) break;
         chunk(k + 2, std::integral_constant<int, 2>{}, NOPAR{});
+      }
+      if constexpr (KU >= 4) {
+        if (k + 3 >= nchunks) break;
+        chunk(k + 3, std::integral_constant<int, 3>{}, NOPAR{});
       }
     }
   }
@@ -465,7 +476,8 @@ __global__ __launch_bounds__(WM * WN * 64, (TH * TW / WM == 32 && BN / WN == 32)
   }
 }
 
-template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0>
+template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0,
+          int OCC = 0, int RF = 0>
 static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   constexpr int NT = WM * WN * 64;
   constexpr int NPA = SplitMode<MODE>::NPA;
@@ -552,7 +564,7 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   }();
   p.ncb = (remap_on && ncb > 1 && blocks % 8 == 0) ? ncb : 0;
   dim3 grid = p.ncb ? dim3((unsigned)(blocks * ncb), 1) : dim3((unsigned)blocks, ncb);
-  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT, GEO, KXT>;
+  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT, GEO, KXT, OCC, RF>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
     status = fail(std::string("split wd conv: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -571,6 +583,11 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   static const bool small1x1 = [] {
     const char* e = getenv("LIC_WD_SMALL1X1");
     return !(e && e[0] == '0');
+  }();
+  // experiment switch (LIC_WD_BN192=1: 16x16 px x 192 ch on 8 waves; =2: on 4 waves, one per SIMD)
+  static const int wd_bn192 = [] {
+    const char* e = getenv("LIC_WD_BN192");
+    return e ? atoi(e) : 0;
   }();
   if (a.mfma_mode != 2 || !a.wgt_split || a.dtype != LIC_F32) return 0;
   if (a.groups != 1 || a.ntaps < 1 || a.force_direct || a.force_mfma_generic) return 0;
@@ -613,6 +630,8 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   if (a.mi > 8 && a.mj > 8 && blocks(16, 16, 64) >= 256) {
     switch (a.ntaps) {
       case 9:   // plain 3x3 stride 1: compile-time addressing (GEO 1); other 3x3 grids (ConvT phases) general
+        if (wd_bn192 == 1 && a.copad == 192 && try_split_wd<2, 9, 16, 16, 192, 4, 2, 3, 0, 1, 0, 2, 2>(a, s, status)) return 1;
+        if (wd_bn192 == 2 && a.copad == 192 && try_split_wd<2, 9, 16, 16, 192, 2, 2, 6, 0, 1, 0, 1, 3>(a, s, status)) return 1;
         if (try_split_wd<2, 9, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status)) return 1;
         return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);
       case 6:   // ConvT phases 3x2 / 2x3 (compile-time grids when the taps ascend), s2 phases general

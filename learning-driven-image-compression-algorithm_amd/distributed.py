@@ -6,15 +6,73 @@ collectives are a barrier around timed regions, a MAX of the elapsed time
 (bench.py) and ONE all-reduce of a small fp64 statistics vector per evaluation
 (eval_net.py: sum of bpp, PSNR, MSE, time and the image count) so that rank 0
 prints exactly the single-process summary.  Backend "nccl" (RCCL over xGMI) on
-the GPU box, "gloo" for the CPU tests.
+the GPU box, "gloo" for the CPU tests.  ``bench.py --gpus N`` / ``eval_net.py --gpus N``
+started without torchrun spawn their N ranks themselves (``launch_workers``).
 """
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
+import sys
+import time
 from typing import List, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+
+
+def launched() -> bool:
+    """True inside a worker of torchrun or of ``launch_workers`` (WORLD_SIZE is set)."""
+    return "WORLD_SIZE" in os.environ
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(cmd: Sequence[str], n: int, poll_s: float = 0.2) -> int:
+    """Run ``cmd`` as ``n`` worker processes, one per GPU, the way ``torch.distributed.run
+    --nnodes 1 --nproc-per-node n`` would: each child gets RANK = LOCAL_RANK = i, WORLD_SIZE =
+    LOCAL_WORLD_SIZE = n and MASTER_ADDR / MASTER_PORT of a local rendezvous; the child selects
+    its device from LOCAL_RANK.  The caller must not have touched the GPU (the children are new
+    programs started with fork + exec of a fresh interpreter; nothing GPU-initialised is ever
+    replaced).  Rank 0's stdout is this process's stdout (the single JSON line of bench.py /
+    eval_net.py); the other ranks' stdout goes to stderr.  When any child fails the others are
+    terminated; returns the first non-zero exit status (0 when every rank succeeded)."""
+    if n < 1:
+        raise ValueError(f"need at least one worker, got {n}")
+    port = _free_port()
+    procs = []
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen(list(cmd), env=env, stdout=None if r == 0 else sys.stderr))
+        status = 0
+        live = set(range(n))
+        while live:
+            for r in sorted(live):
+                rc = procs[r].poll()
+                if rc is None:
+                    continue
+                live.discard(r)
+                if rc != 0 and status == 0:
+                    status = rc
+                    print(f"launch_workers: rank {r} exited with status {rc}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        procs[q].terminate()
+            if live:
+                time.sleep(poll_s)
+        return status
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
 
 
 def env_rank() -> Tuple[int, int, int]:

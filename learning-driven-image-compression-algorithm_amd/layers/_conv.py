@@ -55,10 +55,13 @@ class Conv2d(nn.Conv2d, _PackCache):
             epi: int = EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
             y2: Optional[Act] = None, prologue: int = PRO_NONE, shuffle: bool = False) -> Act:
         k = self.kernel_size[0]
+        square = (self.kernel_size[0] == self.kernel_size[1] and self.stride[0] == self.stride[1] and
+                  (pad is not None or self.padding[0] == self.padding[1]) and self.dilation == (1, 1))
         if (Fn.split_mode() == 2 and x.dtype == torch.float32 and self.groups == 1 and x.c == self.in_channels and
-                x.c <= 4 and 1 < k * k * x.c <= 32 and prologue == PRO_NONE and not shuffle and _PATCHES):
+                x.c <= 4 and 1 < k * k * x.c <= 32 and prologue == PRO_NONE and not shuffle and _PATCHES and square):
             # fp32x6, the image's k x k conv (Cin 3): one 1x1 launch over the patch map (K = 27 -> 32)
-            # instead of k*k taps of a 16-channel-padded input on the exact-fp32 kernel
+            # instead of k*k taps of a 16-channel-padded input on the exact-fp32 kernel (square kernel,
+            # stride and padding only: the patch packer takes one of each)
             if pad is None:
                 p = self.padding[0]
                 pad = (p, p, p, p)

@@ -36,7 +36,7 @@ parameter names ``depthwise`` / ``pointwise``.
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -647,10 +647,15 @@ def counter_noise(seed: int, shape_nhwc) -> Tensor:
 
 
 def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Params, num_slices: int = 4,
-               noise_seed=None):
+               noise_seed=None, forced_symbols: Optional[Tensor] = None):
     """Channel-conditional slice loop, net_ga.py:1021-1067 (eval / dequantize semantics, or with
     noise_seed the training-mode GaussianConditional the reference's eval actually runs:
-    likelihood of y + U(-1/2, 1/2))."""
+    likelihood of y + U(-1/2, 1/2)).
+
+    forced_symbols ([B, 192, h, w] integers, test use): the quantised integers round(y - mu) are
+    replaced by these (y_q = s + mu, y_hat = s + mu + lrp), so the later slices' contexts and every
+    likelihood are evaluated on another path's symbols -- the reference's arithmetic conditioned on
+    that path's near-tie decisions (tests/parity.check_rate)."""
     y_shape = z3.shape[2:]
     y_slices = z3.chunk(num_slices, 1)
     y_hat_slices: List[Tensor] = []
@@ -667,14 +672,20 @@ def slice_loop(z3: Tensor, latent_means: Tensor, latent_scales: Tensor, P: Param
         sc = _conv(gelu(_conv(gelu(_conv(ss, P, f"cc_scale_transforms.{i}.0", 1, 1)), P,
                                    f"cc_scale_transforms.{i}.2", 1, 1)), P, f"cc_scale_transforms.{i}.4", 1, 1)
         sc = sc[:, :, :y_shape[0], :y_shape[1]]
-        if noise_seed is None:
+        forced = None
+        if forced_symbols is not None:
+            c0 = i * y_slice.shape[1]
+            forced = forced_symbols[:, c0:c0 + y_slice.shape[1]].to(mu.dtype)
+        if forced is not None and noise_seed is None:
+            y_q = forced + mu
+        elif noise_seed is None:
             y_q = quantize_dequantize(y_slice, mu)
         else:
             B_, C_, H_, W_ = y_slice.shape
             y_q = y_slice + counter_noise(noise_seed * num_slices + i, (B_, H_, W_, C_)).permute(0, 3, 1, 2)
         lik.append(gaussian_likelihood(y_q, sc, mu))
-        syms.append(symbols(y_slice, mu))
-        y_hat_slice = ste_round(y_slice - mu) + mu
+        syms.append(symbols(y_slice, mu) if forced is None else forced_symbols[:, c0:c0 + y_slice.shape[1]].clone())
+        y_hat_slice = (ste_round(y_slice - mu) if forced is None else forced) + mu
         lrp_support = torch.cat([ms, y_hat_slice], dim=1)
         lrp = _conv(gelu(_conv(gelu(_conv(lrp_support, P, f"lrp_transforms.{i}.0", 1, 1)), P,
                                     f"lrp_transforms.{i}.2", 1, 1)), P, f"lrp_transforms.{i}.4", 1, 1)

@@ -83,3 +83,23 @@ def test_ctypes_struct_offsets_match_c_compiler(tmp_path):
         assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
         for f in py._fields_:
             assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
+
+
+def test_library_built_from_this_tree():
+    """Build provenance: the library's lic_source_hash equals the hash of this tree's csrc/ and
+    include/lic.h (csrc/Makefile SRC_HASH), and lic_version carries it."""
+    lib = lic_amd.load_library()
+    tree = _ffi.source_hash()
+    assert tree is not None and len(tree) == 16
+    assert lib.lic_source_hash().decode() == tree
+    assert f"src {tree}".encode() in lib.lic_version()
+
+
+def test_loader_refuses_a_library_from_other_sources(monkeypatch):
+    """_ffi.load raises LicError when the tree's sources differ from the ones the .so was built from."""
+    import pytest
+    monkeypatch.setattr(_ffi, "_lib", None)
+    monkeypatch.setattr(_ffi, "_load_error", None)
+    monkeypatch.setattr(_ffi, "source_hash", lambda: "0000000000000000")
+    with pytest.raises(_ffi.LicError, match="built from other sources"):
+        _ffi.load()

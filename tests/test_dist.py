@@ -120,3 +120,48 @@ def test_grad_allreduce_single_process_noop():
     p.grad = torch.full((3,), 2.0)
     D.GradAllReduce([p], 1).finish()
     assert torch.equal(p.grad, torch.full((3,), 2.0))
+
+
+def test_bench_launcher_two_ranks_dry_run():
+    """`python bench.py --gpus 2` without torchrun starts its two ranks itself (gloo, --dry-run:
+    no CUDA call), and rank 0's single JSON line reports n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3"],
+                         capture_output=True, text=True, timeout=180, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]   # (gloo logs its connections)
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["global_batch"] == 64 and rec["steps"] == 3 and rec["dry_run"]
+
+
+def test_launch_workers_propagates_failure():
+    """A failing rank stops the others and its exit status is returned."""
+    import sys
+    import time
+    code = ("import os, sys, time\n"
+            "r = int(os.environ['RANK'])\n"
+            "assert os.environ['WORLD_SIZE'] == '3' and os.environ['LOCAL_RANK'] == str(r)\n"
+            "assert os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+            "sys.exit(7) if r == 2 else time.sleep(60)\n")
+    t0 = time.time()
+    assert D.launch_workers([sys.executable, "-c", code], 3) == 7
+    assert time.time() - t0 < 30
+    ok = "import os; assert int(os.environ['WORLD_SIZE']) == 2"
+    assert D.launch_workers([sys.executable, "-c", ok], 2) == 0
+
+
+def test_bench_rejects_world_mismatch():
+    """Under torchrun, --gpus must equal the launched world size."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode != 0 and "launcher started 1 ranks" in out.stderr

@@ -186,7 +186,7 @@ def test_truncated_stream_is_flagged_not_fatal():
         EC.from_strings([EC.to_strings(words, offsets, 1, 1)[0][:-4]], 1, DEV)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp16", "fp32x6"])
 def test_net_compress_decompress_round_trip(precision):
     from lic_amd.model import net_ga
     torch.manual_seed(0)
@@ -206,6 +206,39 @@ def test_net_compress_decompress_round_trip(precision):
     bpp_real = nbits / (2 * 256 * 256)
     print(f"\n[{precision}] estimated y bpp {bpp.item():.4f}, coded (y+z, incl. headers) {bpp_real:.4f}")
     assert bpp_real > 0.9 * bpp.item()
+
+
+def test_net_compress_decompress_fp32x6_b32_fresh_decoder():
+    """The headline precision at the bench batch: compress 32 images with one Net, decode the
+    strings with a second Net built from the same state_dict (fresh weight packs, split caches and
+    buffers: nothing shared with the encoder), and require the decoder's symbols and
+    reconstruction to equal the encoder-side forward's bitwise -- the split kernels are
+    deterministic across instances and calls (encoder / decoder agree on every scale index)."""
+    from lic_amd.model import net_ga
+    B = 32
+    torch.manual_seed(0)
+    enc_net = net_ga.synthetic_syntax_bias_(
+        net_ga.Net((B, 256, 256, 3), (B, 256, 256, 3), False, False, precision="fp32x6")).to(DEV)
+    x = (torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1000)) * 2 - 1).to(DEV)
+    bpp, v_mse, v_psnr = enc_net(x, "test", return_intermediates=True)
+    fwd_sym = enc_net.last["symbols"].permute(0, 2, 3, 1).cpu()
+    fwd_rec = enc_net.last["x_rec"].cpu()
+    enc = enc_net.compress(x)
+    assert torch.equal(enc["symbols"].cpu(), fwd_sym)
+    sd = {k: v.detach().cpu().clone() for k, v in enc_net.state_dict().items()}
+    del enc_net
+    torch.cuda.empty_cache()
+    dec_net = net_ga.Net((B, 256, 256, 3), (B, 256, 256, 3), False, False, precision="fp32x6")
+    dec_net.load_state_dict(sd)
+    dec_net = dec_net.to(DEV)
+    dec = dec_net.decompress(enc["strings"], enc["shape"], enc["syntax"])
+    assert torch.equal(dec["symbols"].cpu(), fwd_sym)
+    assert torch.equal(dec["x_hat"].cpu(), fwd_rec)
+    dec2 = dec_net.decompress(enc["strings"], enc["shape"], enc["syntax"])
+    assert torch.equal(dec2["x_hat"].cpu(), fwd_rec)
+    nbits = 8 * sum(len(s) for lst in enc["strings"] for s in lst)
+    print(f"\n[fp32x6 B=32] estimated y bpp {bpp.item():.4f}, coded {nbits / (B * 65536):.4f}")
+    assert nbits / (B * 65536) > 0.9 * bpp.item()
 
 
 def test_unet_ha_hs_is_not_codable():

@@ -11,15 +11,17 @@ CPU oracle (oracle/ref_cpu.py, fp32 torch CPU):
          fp32-summation-order near-ties (tests/parity.py), bpp within 1e-5, PSNR within 1e-4 dB.
   cfg 3: net_unet_ha_hs encode -> quantize -> decode, 16 x 512^2, fp32: same bars, and the
          reconstruction within one uint8 step.
+Both forwards run twice: exact fp32 and fp32x6 (the bench headline's precision: fp32
+activations and accumulation, six bf16 products of exact three-part splits per product), each
+against the same oracle run; the rate bar is tests/parity.check_rate (1e-5 bpp against the oracle
+conditioned on the path's own symbols, the measured bits of flipped near-ties reported beside it).
 Weights: seeded reference init + net_ga.synthetic_syntax_bias_ (non-degenerate x_rec).
 """
-import math
-
 import pytest
 import torch
 
 from oracle import ref_cpu as R
-from parity import check_decoder, check_symbols
+from parity import check_decoder, check_flip_sets_match, check_rate, check_symbols
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -50,32 +52,48 @@ def test_cfg2_analysis_b32_fp16():
     assert err.max().item() < 2e-2
 
 
-def _compare_forward(arch, B, S, seed, xseed):
-    net = _net(arch, "fp32", B, S, seed)
-    P = {k: v.detach().float() for k, v in net.state_dict().items()}
+def _check_precision(arch, prec, B, S, net0, x, ref, P):
+    """One precision's forward against the oracle: symbols (near-tie rule), rate by
+    tests/parity.check_rate (1e-5 bpp against the oracle on the same symbols, batch and per image),
+    PSNR 1e-4 dB (batch, and per image on the flip-free images), decoder pinned.  Returns the flip mask."""
+    net = _net(arch, prec, B, S)
+    net.load_state_dict(net0.state_dict())
     net = net.to(DEV)
-    x = _x(B, S, xseed)
     bpp, v_mse, v_psnr = net(x.to(DEV), "test", return_intermediates=True)
     torch.cuda.synchronize()
-    ref = R.net_forward(x, P, arch=arch)
     flips = check_symbols(net.last["symbols"], ref)
-    # per-image rate from the likelihoods (bpp of net_ga.py:1134 restricted to one image)
-    lik = net.last["likelihoods"].double().cpu()
-    hw = S * S
-    bpp_img = -torch.log(lik).sum(dim=(1, 2, 3)) / (math.log(2) * hw)
-    bpp_img_ref = -torch.log(ref["likelihoods"].double()).sum(dim=(1, 2, 3)) / (math.log(2) * hw)
-    d_img = (bpp_img - bpp_img_ref).abs().max().item()
+    flipped = net.last["symbols"].cpu() != ref["symbols"]
+    rate = check_rate(net.last["likelihoods"], ref, net.last["symbols"], P, bpp.item(), S * S)
     psnr_img = 20 * torch.log10(255 / torch.sqrt(v_mse.double().cpu()))
     psnr_img_ref = 20 * torch.log10(255 / torch.sqrt(ref["v_mse"].double()))
-    print(f"\n[{arch} fp32 B={B} {S}^2] flips {flips} d_bpp {abs(bpp.item() - ref['bpp'].item()):.2e} "
-          f"(per image max {d_img:.2e}) d_psnr {abs(v_psnr.item() - ref['v_psnr'].item()):.2e} "
-          f"(per image max {(psnr_img - psnr_img_ref).abs().max().item():.2e})")
-    # bpp bar 1e-5, widened by 64 bits per flipped near-tie symbol (tests/parity.py)
-    assert abs(bpp.item() - ref["bpp"].item()) <= 1e-5 * max(1.0, abs(ref["bpp"].item())) + flips * 64.0 / (B * hw)
-    assert d_img <= 1e-5 * max(1.0, bpp_img_ref.abs().max().item()) + flips * 64.0 / hw
+    # per-image PSNR vs the free-running oracle on the images without a flipped symbol; an image with
+    # one decodes another y_hat there and is pinned on its own y_hat by check_decoder
+    clean = ~flipped.flatten(1).any(1)
+    d_img = (psnr_img - psnr_img_ref).abs()[clean]
+    print(f"\n[{arch} {prec} B={B} {S}^2] flips {flips} d_bpp {rate['d_bpp']:.2e} (same symbols "
+          f"{rate['d_bpp_same_symbols']:.2e}, per image max {rate['d_bpp_per_image']:.2e}; flip bits "
+          f"{rate['flip_bits']:.2f}) d_psnr {abs(v_psnr.item() - ref['v_psnr'].item()):.2e} "
+          f"(per flip-free image max {d_img.max().item() if d_img.numel() else 0.0:.2e}, {int(clean.sum())} images)")
     assert abs(v_psnr.item() - ref["v_psnr"].item()) <= 1e-4
-    assert (psnr_img - psnr_img_ref).abs().max().item() <= 1e-4
+    assert d_img.numel() == 0 or d_img.max().item() <= 1e-4
     check_decoder(net.last, ref, P, flips)
+    del net
+    torch.cuda.empty_cache()
+    return flipped
+
+
+def _compare_forward(arch, B, S, seed, xseed, precisions=("fp32", "fp32x6")):
+    """The exact-fp32 path and the headline's fp32x6 path on the same weights and batch, against
+    one oracle run; the two fp32-grade paths flip the same symbols up to oracle ties within 1e-6
+    of the .5 boundary and their cascades (tests/parity.check_flip_sets_match)."""
+    net0 = _net(arch, "fp32", B, S, seed)
+    P = {k: v.detach().float() for k, v in net0.state_dict().items()}
+    x = _x(B, S, xseed)
+    ref = R.net_forward(x, P, arch=arch)
+    masks = {p: _check_precision(arch, p, B, S, net0, x, ref, P) for p in precisions}
+    if "fp32" in masks and "fp32x6" in masks:
+        n = check_flip_sets_match(masks["fp32x6"], masks["fp32"], ref)
+        print(f"flip-set difference fp32x6 vs exact fp32: {n}")
 
 
 def test_cfg2_forward_b32_fp32_bit_exact_symbols():

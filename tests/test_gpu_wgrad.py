@@ -25,8 +25,7 @@ def _check(dw, ref, name):
     assert err <= 2e-5 * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("B,H,W,ci,co,k,s,pad", [
+SHAPES = [
     (2, 20, 24, 64, 64, 3, 1, (1, 1, 1, 1)),       # ragged 8x8 tiles
     (1, 16, 16, 192, 128, 3, 1, (1, 1, 1, 1)),     # 3 x 2 channel blocks
     (2, 12, 10, 96, 40, 3, 1, (1, 1, 1, 1)),       # partial 64-wide blocks on both sides
@@ -41,7 +40,11 @@ def _check(dw, ref, name):
     (1, 10, 10, 32, 64, 7, 2, (3, 3, 3, 3)),       # 7x7 s2
     (1, 11, 13, 32, 48, 2, 1, (0, 0, 1, 1)),       # 2x2: the generic kernel
     (1, 9, 9, 16, 64, 1, 2, (0, 0, 0, 0)),         # 1x1 s2
-])
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,H,W,ci,co,k,s,pad", SHAPES)
 def test_conv_wgrad(dtype, B, H, W, ci, co, k, s, pad):
     from lic_amd import autograd as AG
     g = torch.Generator().manual_seed(B * 1000 + H * 31 + ci + co + k + s)
@@ -119,3 +122,40 @@ def test_wgrad_config5_split_k(dtype, C, HW):
     torch.cuda.synchronize()
     ref = torch.nn.grad.conv2d_weight(_nchw(x).double(), (C, C, 3, 3), _nchw(dz).double(), padding=1)
     _check(dw, ref, "wgrad config5")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("B,H,W,ci,co,k,s,pad", SHAPES + [
+    (8, 32, 32, 192, 192, 3, 1, (1, 1, 1, 1)),     # config 5's 192-channel 3x3 (split K over many tiles)
+    (2, 16, 16, 64, 200, 3, 1, (1, 1, 1, 1)),      # co = 3 x 64 + 8: a ragged last co block
+])
+def test_conv_wgrad_fused_bias(dtype, B, H, W, ci, co, k, s, pad):
+    """The bias gradient of the same launch (lic_wgrad_args.db: per-split dz column sums finished by
+    the split reduce on the tiled 16-bit kernel, the channel-sum pass on the generic / fp32 path)
+    against float64 sum_pix dz[pix, n]; then a second launch with accumulate=1 adds both dW and db
+    onto what is there."""
+    from lic_amd import autograd as AG
+    g = torch.Generator().manual_seed(B * 977 + H * 13 + ci + 3 * co + k + s)
+    pt, pl, pb, pr = pad
+    Ho = (H + pt + pb - k) // s + 1
+    Wo = (W + pl + pr - k) // s + 1
+    x = torch.randn(B, H, W, ci, generator=g).to(dtype)
+    dz = torch.randn(B, Ho, Wo, co, generator=g).to(dtype)
+    dw = torch.empty((co, ci, k, k), dtype=torch.float32, device=DEV)
+    db = torch.full((co,), float("nan"), dtype=torch.float32, device=DEV)
+    tdy, tdx = AG._taps(k, k, pt, pl)
+    AG.wgrad(x.to(DEV), dz.to(DEV), tdy, tdx, stride=s, dw=dw, strides=(ci * k * k, k * k, 1), co_out=co,
+             ci_out=ci, db=db)
+    torch.cuda.synchronize()
+    xp = torch.nn.functional.pad(_nchw(x).double(), (pl, pr, pt, pb))
+    ref = torch.nn.grad.conv2d_weight(xp, (co, ci, k, k), _nchw(dz).double(), stride=s)
+    ref_b = dz.double().sum(dim=(0, 1, 2))
+    _check(dw, ref, f"wgrad k{k} s{s} (with db)")
+    _check(db, ref_b, f"db k{k} s{s}")
+    base_b = torch.randn(co, generator=g)
+    db.copy_(base_b)
+    AG.wgrad(x.to(DEV), dz.to(DEV), tdy, tdx, stride=s, dw=dw, strides=(ci * k * k, k * k, 1), co_out=co,
+             ci_out=ci, db=db, accumulate=True)
+    torch.cuda.synchronize()
+    _check(dw, 2 * ref, f"wgrad k{k} s{s} accumulate")
+    _check(db - base_b.to(DEV), ref_b, f"db k{k} s{s} accumulate")

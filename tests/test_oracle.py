@@ -189,3 +189,28 @@ def test_counter_noise_is_uniform_and_seeded():
     assert abs(u.mean().item()) < 0.02 and abs(u.var().item() - 1 / 12) < 0.01
     assert torch.equal(u, R.counter_noise(3, (2, 8, 8, 48)))
     assert not torch.equal(u, R.counter_noise(4, (2, 8, 8, 48)))
+
+
+def test_slice_loop_forced_symbols():
+    """oracle.slice_loop(forced_symbols=...): forcing the oracle's own symbols reproduces its
+    likelihoods bitwise; forcing one flipped symbol of slice 0 changes that symbol's likelihood
+    and the contexts (mu / sigma) of later slices only, never an earlier or the same slice's
+    other symbols (tests/parity.check_rate conditions the oracle on a GPU path's symbols)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as MG
+    P = MG.state_of(MG.make_net("net_ga", 256, 0))
+    x = MG.seeded_image(1, 256, 3)
+    ref = R.net_forward(x, P, arch="net_ga")
+    args = (ref["z3"], ref["latent_means"], ref["latent_scales"], P)
+    _, lik, sym, mu, sc = R.slice_loop(*args, forced_symbols=ref["symbols"].to(torch.int32))
+    assert torch.equal(lik, ref["likelihoods"]) and torch.equal(mu, ref["means"]) and torch.equal(sc, ref["scales"])
+    forced = ref["symbols"].to(torch.int32).clone()
+    forced[0, 5, 1, 2] += 1
+    _, lik2, sym2, mu2, sc2 = R.slice_loop(*args, forced_symbols=forced)
+    assert torch.equal(sym2, forced)
+    changed = lik2 != lik
+    assert changed[0, 5, 1, 2]
+    assert not changed[:, :48].flatten()[torch.arange(48 * 256) != (5 * 256 + 1 * 16 + 2)].any()
+    assert torch.equal(mu2[:, :48], mu[:, :48]) and not torch.equal(mu2[:, 48:], mu[:, 48:])

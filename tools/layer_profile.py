@@ -57,6 +57,9 @@ def wrap(name):
             mi, mj = kw.get("out_hw") or (out.H, out.W)
             if kw.get("shuffle") is True:
                 mi, mj = out.H // 2, out.W // 2
+            if pk.phase is not None:   # a transposed-conv phase computes every s-th output pixel only
+                ry, rx, s = pk.phase[0], pk.phase[1], pk.phase[2]
+                mi, mj = -(-(out.H - ry) // s), -(-(out.W - rx) // s)
             r[2] += 2.0 * out.B * mi * mj * pk.co * pk.ci * len(pk.dy) / max(1, pk.groups)
         return out
     setattr(Fn, name, w)
