@@ -642,6 +642,7 @@ int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
         return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status) || try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);
       case 2: return try_split_wd<2, 2, 16, 16, 64, 2, 2, 6>(a, s, status);     // 3x3 s2 phases 2x1 / 1x2
       case 49:   // 7x7: 8 waves, 22x22 halo
+        if (wd_bn192 == 1 && a.copad == 192 && try_split_wd<2, 49, 16, 16, 192, 4, 2, 4, 0, 1, 0, 2, 2>(a, s, status)) return 1;
         return try_split_wd<2, 49, 16, 16, 64, 4, 2, 4, 0, 1>(a, s, status) || try_split_wd<2, 49, 16, 16, 64, 4, 2, 4>(a, s, status);
       default: break;
     }

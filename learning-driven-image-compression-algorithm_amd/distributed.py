@@ -138,10 +138,17 @@ class GradAllReduce:
     overlapping the rest of the backward.  ``finish()`` launches what is left (buckets
     holding parameters that got no gradient this step: only the ones that did are reduced,
     the same set on every rank because every rank runs the same graph), waits, divides by
-    the world size and scatters back into ``.grad``."""
+    the world size and scatters back into ``.grad``.
 
-    def __init__(self, params, world: int, bucket_mb: float = 32.0):
+    Every step of it is stream-ordered (flatten, RCCL all-reduce on the communicator's stream
+    joined through events, wait, scale, scatter), so a training step that calls ``finish()``
+    inside ``torch.cuda.graph`` captures the collectives too: replays run the bucketed all-reduce
+    with no host work (train_net_unet.py --graph at world > 1).  ``force`` runs the collective
+    path at world 1 as well (a one-rank all-reduce: the graph-capture test of the path)."""
+
+    def __init__(self, params, world: int, bucket_mb: float = 32.0, force: bool = False):
         self.world = world
+        self.active = world > 1 or force
         self.params = [p for p in params if p.requires_grad]
         buckets, cur, size = [], [], 0
         for p in reversed(self.params):
@@ -159,7 +166,7 @@ class GradAllReduce:
         self._flat = [None] * len(buckets)
         self._members = [None] * len(buckets)
         self._hooks = []
-        if world > 1:
+        if self.active:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
@@ -180,7 +187,7 @@ class GradAllReduce:
 
     def finish(self) -> None:
         """Complete every bucket's all-reduce and write the averaged gradients back."""
-        if self.world <= 1:
+        if not self.active:
             return
         for i in range(len(self.buckets)):
             if self._members[i] is None:

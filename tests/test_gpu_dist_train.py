@@ -84,3 +84,80 @@ def test_grad_allreduce_on_liblic_model_two_ranks():
         assert np.array_equal(a, b)                     # both ranks hold the same averaged gradient
         mean = (g0.astype(np.float32) + g1.astype(np.float32)) / np.float32(2)
         assert np.allclose(a, mean, rtol=0, atol=1e-6 * (np.abs(mean).max() + 1e-30))
+
+
+def _graph_worker(port, q):
+    """One rank with the RCCL ("nccl") backend: the training step with GradAllReduce's bucketed
+    all-reduce (force=True runs the collective path at world 1) eager, and the same step captured
+    in a hipGraph (train_net_unet.py --graph at world > 1) and replayed."""
+    import copy
+    import torch.distributed as dist
+    from lic_amd import distributed as D
+    from lic_amd.model import net_ga, net_unet_ha_hs
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    torch.manual_seed(0)
+    base = net_ga.synthetic_syntax_bias_(net_unet_ha_hs.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False,
+                                                            precision="bf16"))
+    x = (torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(9)) * 2 - 1).to("cuda")
+    steps = 3
+
+    def make():
+        net = copy.deepcopy(base).to("cuda")
+        params = net.base_params()
+        opt = torch.optim.Adam(params, lr=torch.tensor(1e-4, device="cuda"), capturable=True)
+        sync = D.GradAllReduce(params, 1, bucket_mb=4.0, force=True)
+        return net, params, opt, sync, torch.zeros((1,), dtype=torch.int64, device="cuda")
+
+    def body(net, params, opt, sync, seed_t):
+        bpp, mse = net(x, "train", seed_dev=seed_t)
+        loss = 0.0025 * 255 ** 2 * mse + bpp
+        loss.backward()
+        sync.finish()
+        torch.nn.utils.clip_grad_norm_([p for p in params if p.grad is not None], 1.0)
+        opt.step()
+        seed_t.add_(1)
+        return loss.detach()
+
+    net_a, pa, oa, sa_, ta = make()
+    losses_a = []
+    for _ in range(steps):
+        oa.zero_grad(set_to_none=True)
+        losses_a.append(body(net_a, pa, oa, sa_, ta).item())
+    launched = len(sa_.buckets)
+    net_b, pb, ob, sb_, tb = make()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ob.zero_grad(set_to_none=True)
+        first = body(net_b, pb, ob, sb_, tb).item()
+    torch.cuda.current_stream().wait_stream(side)
+    ob.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        out = body(net_b, pb, ob, sb_, tb)
+    losses_b = [first]
+    for _ in range(steps - 1):
+        g.replay()
+        losses_b.append(out.item())
+    torch.cuda.synchronize()
+    d = max(((p - q).norm() / (p.norm() + 1e-12)).item() for p, q in zip(net_a.parameters(), net_b.parameters()))
+    q.put((losses_a, losses_b, d, launched))
+    del g
+    dist.destroy_process_group()
+
+
+def test_graph_step_with_rccl_allreduce_matches_eager():
+    """train_net_unet.py --graph at world > 1: the bucketed RCCL all-reduce is captured with the
+    backward (a world-1 "nccl" group, collectives forced on); the replayed steps equal the eager
+    steps bitwise (losses and every parameter)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_worker, args=(_free_port(), q))
+    p.start()
+    losses_a, losses_b, d, nb = q.get(timeout=300)
+    p.join(timeout=60)
+    print(f"\n[graph + RCCL all-reduce, {nb} buckets] eager losses {losses_a}, graph losses {losses_b}, "
+          f"max relative parameter difference {d:.2e}")
+    assert p.exitcode == 0
+    assert losses_a == losses_b and d == 0

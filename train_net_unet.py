@@ -79,21 +79,29 @@ def main():
     ap.add_argument("--bench", action="store_true", help="time --steps steps after --warmup, print JSON")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--gpus", type=int, default=1, help="informational; world size comes from torchrun")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without torchrun this process starts them itself")
     ap.add_argument("--graph", action="store_true",
-                    help="capture the whole step (forward, backward, clip, Adam) in one hipGraph and replay it: "
-                         "no per-launch host cost; the noise seed lives on the device (bf16 / fp32, one GPU; "
-                         "the default there)")
+                    help="capture the whole step (forward, backward, RCCL gradient all-reduce, clip, Adam) in "
+                         "one hipGraph and replay it: no per-launch host cost; the noise seed lives on the device "
+                         "(bf16 / fp32, any world size; the default there)")
     ap.add_argument("--eager", action="store_true", help="run every step eagerly (no hipGraph capture)")
     args = ap.parse_args()
 
     from lic_amd import distributed as D
+    if args.gpus > 1 and not D.launched():
+        # one process per GPU, started before this process touches the GPU (no re-exec)
+        sys.exit(D.launch_workers([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
     from lic_amd.model import net_ga, net_unet_ha_hs
     rank, world, local = D.init("nccl")
-    # one GPU, bf16 / fp32: the captured step is the default (replays equal the eager steps,
-    # tests/test_gpu_train_net.py::test_train_step_hipgraph_matches_eager); ~7000 launches per step
-    # otherwise leave the GPU waiting on the host
-    args.graph = not args.eager and (args.graph or (world == 1 and args.precision != "fp16"))
+    if D.launched() and args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"train_net_unet.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    # bf16 / fp32: the captured step is the default, on one GPU and on N (the bucketed RCCL gradient
+    # all-reduce is captured with the backward; replays equal the eager steps,
+    # tests/test_gpu_train_net.py::test_train_step_hipgraph_matches_eager,
+    # tests/test_gpu_dist_train.py::test_graph_step_with_rccl_allreduce_matches_eager); ~7000 launches
+    # per step otherwise leave the GPU waiting on the host
+    args.graph = not args.eager and (args.graph or args.precision != "fp16")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B = int(args.batch_size)
@@ -106,9 +114,8 @@ def main():
         net.load_state_dict(torch.load(args.weight_path, map_location="cpu", weights_only=True), strict=True)
     net = net.to(dev)
     params = net.base_params()
-    if args.graph and (args.precision == "fp16" or world > 1):
-        raise SystemExit("--graph: bf16 / fp32 on one GPU (GradScaler syncs the host; the grad all-reduce is "
-                         "not captured)")
+    if args.graph and args.precision == "fp16":
+        raise SystemExit("--graph: bf16 / fp32 (fp16's GradScaler syncs the host every step)")
     # capturable Adam keeps lr and the step count on the device (graph replays update them)
     opt = torch.optim.Adam(params, lr=torch.tensor(args.lr, device=dev) if args.graph else args.lr,
                            capturable=args.graph)
@@ -123,6 +130,7 @@ def main():
         bpp, mse = net(x, "train", seed_dev=seed_dev)
         loss = args.lmbda * 255 ** 2 * mse + bpp                       # :180
         loss.backward()
+        sync.finish()                                                  # RCCL all-reduce, captured too
         torch.nn.utils.clip_grad_norm_(grad_params, 1.0)               # :198
         opt.step()
         return loss.detach(), bpp.detach(), mse.detach()
@@ -138,6 +146,7 @@ def main():
                 opt.zero_grad(set_to_none=True)
                 bpp, mse = net(static_x, "train", seed_dev=seed_t)
                 (args.lmbda * 255 ** 2 * mse + bpp).backward()
+                sync.finish()              # first collectives eagerly: communicator set up before capture
                 grad_params = [p for p in params if p.grad is not None]
                 torch.nn.utils.clip_grad_norm_(grad_params, 1.0)
                 opt.step()
