@@ -24,6 +24,8 @@ SHAPES = [
     ("conv5x5s2@128", 192, 192, 5, 2, (1, 1, 2, 2), 128),
     ("conv5x5s2@32", 192, 192, 5, 2, (1, 1, 2, 2), 32),
     ("qkv1x1@64", 192, 576, 1, 1, (0, 0, 0, 0), 64),
+    ("proj1x1@64", 192, 192, 1, 1, (0, 0, 0, 0), 64),
+    ("c1x1@128", 192, 192, 1, 1, (0, 0, 0, 0), 128),
     ("rbneck3x3_96@64", 96, 96, 3, 1, (1, 1, 1, 1), 64),
     ("han3x3_64@256", 64, 64, 3, 1, (1, 1, 1, 1), 256),
     # slice loop / hyper shapes on the 16x16 latent
