@@ -142,9 +142,16 @@ static int conv_dispatch(const lic_conv_args& a, hipStream_t s) {
   const int64_t out_pix = (int64_t)a.n * a.ho * a.wo;
   if (M64 >= (1LL << 31) || out_pix >= (1LL << 31)) return fail("conv: too many pixels for int32 indexing");
   const int M = (int)M64;
-  bool mfma_ok = !a.force_direct && a.groups == 1 && a.prologue != LIC_PRO_ABS && a.ci % EPC == 0 && a.cpad % BK == 0 &&
-                 a.ldx % EPC == 0 && ((uintptr_t)a.x % 16 == 0) && ((uintptr_t)a.wgt % 16 == 0) &&
-                 a.copad % 32 == 0 && a.ci >= EPC;
+  // the halo kernel takes any multiple of its 32-byte chunk (2 * EPC channels: one 8-channel fp32 chunk
+  // for the padded image); the split and generic MFMA kernels want 4 * EPC
+  const bool tile_ok = !a.force_direct && a.groups == 1 && a.prologue != LIC_PRO_ABS && a.ci % EPC == 0 &&
+                       a.cpad % (2 * EPC) == 0 && a.ldx % EPC == 0 && ((uintptr_t)a.x % 16 == 0) &&
+                       ((uintptr_t)a.wgt % 16 == 0) && a.copad % 32 == 0 && a.ci >= EPC;
+  bool mfma_ok = tile_ok && a.cpad % BK == 0;
+  if (tile_ok && !mfma_ok && !a.force_mfma_generic) {
+    int st = 0;
+    if (conv_halo_dispatch<T>(a, s, st)) return st;
+  }
   if (mfma_ok && !a.force_mfma_generic) {
     int st = 0;
     if constexpr (sizeof(T) == 4) {

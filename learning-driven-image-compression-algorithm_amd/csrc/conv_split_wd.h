@@ -70,28 +70,26 @@ struct WdPlan {
 // address VALU of the general path (~5 per ds_read, half of the kernel's vector instructions,
 // profiles/r03/wd_ablation_pmc.txt) is gone.
 // OCC: waves per SIMD the registers are budgeted for (0: four for the one-tile-per-wave small-map
-// configurations, else two); RF: B-ring slots (0: by the tap count, below)
+// configurations, else two); RF: B-ring slots (0: by the tap count, below).
+// KS = 2: two tap groups ("tap split").  The workgroup has 2 x WM x WN waves; group g runs taps
+// [T0, TE) (the first / second half of the tap grid) of every chunk on its own accumulators, both
+// groups share the chunk's halo planes, its split work and its barrier, and group 1 hands its sums
+// to group 0 through LDS at the end (one add per accumulator).  Each wave's dependent MFMA chain is
+// half as long and the launch has twice the waves: for latency-bound grids (the 16x16 latents of the
+// slice loop, fewer workgroups than the GPU holds) that is what bounds the step.
 template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0,
-          int OCC = 0, int RF = 0>
-__global__ __launch_bounds__(WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 && BN / WN == 32) ? 4 : 2)) void conv_split_wd_kernel(
+          int OCC = 0, int RF = 0, int KS = 1>
+__global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 && BN / WN == 32) ? 4 : 2)) void conv_split_wd_kernel(
     const lic_conv_args a, const WdPlan p) {
   using SM = SplitMode<MODE>;
   using T = typename SM::T;
   constexpr int NPA = SM::NPA, NPB = SM::NPB, NPROD = SM::NPROD;
-  constexpr int NT = WM * WN * 64;
+  constexpr int NT = KS * WM * WN * 64;
   constexpr int BM = TH * TW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  // chunks unrolled per loop trip so that the B-ring slot of every step is a compile-time index
-  // B ring: R slots, B(s+2) issued at step s into slot (s+2) % R.  R divides NTAPS where it can (3 or
-  // 4), so every chunk starts at slot 0; else the chunk loop is unrolled by KU = 3 (chunk k starts
-  // at slot (k*NTAPS) % 3)
-  // (an even tap count that 3 and 4 do not divide: two slots at prefetch distance one)
-  constexpr int R = RF > 0 ? RF : ((NTAPS % 3 == 0) ? 3 : ((NTAPS % 4 == 0) ? 4 : ((NTAPS % 2 == 0) ? 2 : 3)));
-  constexpr int PD = R == 2 ? 1 : 2;   // B prefetch distance in steps
-  // chunks per loop trip: the smallest KU with KU * NTAPS a multiple of R
-  constexpr int KU = (NTAPS % R == 0) ? 1 : ((2 * NTAPS) % R == 0 ? 2 : ((3 * NTAPS) % R == 0 ? 3 : 4));
-  static_assert((KU * NTAPS) % R == 0, "B ring");
+  static_assert(KS == 1 || (KS == 2 && GEO == 1 && VT == 0 && NTAPS >= 2 && TM * TN <= 4),
+                "tap groups: compile-time tap grids, accumulators staged whole");
   constexpr int CSTEP = 16 * (VT > 0 ? VT : 1);   // input channels per chunk
   static_assert(WTM % 32 == 0 && WTN % 32 == 0 && NT % 4 == 0, "tile");
   static_assert(VT == 0 || VT == NTAPS, "virtual taps");
@@ -117,7 +115,9 @@ __global__ __launch_bounds__(WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 
   float* sbias = (float*)(rowpix + BM);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar wave offsets (no waterfall loops)
-  const int wm = wave / WN, wn = wave % WN;
+  const int kg = KS > 1 ? wave / (WM * WN) : 0;           // tap group
+  const int wl = KS > 1 ? wave - kg * (WM * WN) : wave;   // wave within the group
+  const int wm = wl / WN, wn = wl % WN;
   const int lrow = lane & 31, lhalf = lane >> 5;
 
   // XCD-aware order (p.ncb > 0): workgroups are dealt round-robin to the 8 XCDs, so id, id + 8, ...
@@ -306,8 +306,8 @@ __global__ __launch_bounds__(WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 
   // A: ONE register set; each part is re-read for the next tap right after this tap's last product
   // that reads it (products run smallest first, pr = NPROD-1 .. 0, so part NPA-1 is free after the
   // first group and part 0 is needed first only by the third), so the reads have most of a step
-  // to land.  B: a ring of R slots by step, B(s+2) issued at step s.
-  u32x4 fa[NPA][TM], fb[R][NPB][TN];
+  // to land.  B: a ring of R slots by step, B(s+2) issued at step s (below, per tap group).
+  u32x4 fa[NPA][TM];
   // one tap's products; the running sum is the MFMA's C operand.  `mid` runs after the first product
   // group: the next chunk's split work of this step, interleaved with the MFMAs by the scheduler
   auto step = [&](const char* set, int toff_next, bool has_next, const u32x4(&fbc)[NPB][TN], auto&& mid) {
@@ -343,116 +343,160 @@ __global__ __launch_bounds__(WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 
     split_quad(i, 1.f, smem);
     load_quad(i, 1 < nchunks ? 1 : 0);
   }
-#pragma unroll
-  for (int q = 0; q < PD; ++q) load_b(q, fb[q]);
-  __syncthreads();
 
-  // one chunk; KS = chunk index mod KU (compile-time), so step s = k*NTAPS + t sits in ring slot
-  // (KS*NTAPS + t) % R.  During chunk k, step t also splits halo quads [t*QPS, (t+1)*QPS) of chunk
-  // k+1 (in the registers since chunk k-1) into the other plane set -- free since the barrier that
-  // ended chunk k-1 -- and refills those registers with chunk k+2: the split's VALU work and its LDS
-  // stores sit between this wave's MFMAs instead of in a serial phase before the barrier.
-  constexpr int QPS = (NQ + NTAPS - 1) / NTAPS;
-  // PAR: chunks unrolled in pairs so that a chunk's parity (its plane set, the next chunk's sign) is
-  // a compile-time constant: the sign folds into the split's instructions, the set into LDS offsets
-  constexpr bool PAR = FIX && KU == 1 && NTAPS <= 9 && TW == 8;   // (16-wide: the pair spills)
-  auto chunk = [&](int k, auto ks, auto kpar) {
-    constexpr int KS = decltype(ks)::value;
-    constexpr int KP = decltype(kpar)::value;   // k & 1 when >= 0
-    const int kodd = KP >= 0 ? KP : (k & 1);
-    const char* set = smem + kodd * SET;
-    char* nset = smem + (kodd ^ 1) * SET;
-    const float nsg = WD_ALT ? (kodd ? 1.f : -1.f) : 1.f;   // sign of chunk k + 1
-    const int kn = k + 2 < nchunks ? k + 2 : nchunks - 1;
+  // the chunk loop of tap group G (taps [T0, TE) of every chunk; KS = 1: all taps)
+  auto run_group = [&](auto gi) {
+    constexpr int G = decltype(gi)::value;
+    constexpr int T1 = KS > 1 ? (NTAPS + 1) / 2 : NTAPS;
+    constexpr int T0 = G == 0 ? 0 : T1, TE = G == 0 ? T1 : NTAPS;
+    constexpr int NTG = TE - T0;   // taps per chunk of this group = its steps per chunk
+    // B ring: R slots, B(l+PD) issued at the group's step l into slot (l+PD) % R.  R divides NTG
+    // where it can (3 or 4), so every chunk starts at slot 0; else the chunk loop is unrolled by KU
+    // (chunk k starts at slot (k*NTG) % R); an even count that 3 and 4 do not divide: two slots at
+    // prefetch distance one
+    constexpr int R = (KS == 1 && RF > 0) ? RF : ((NTG % 3 == 0) ? 3 : ((NTG % 4 == 0) ? 4 : ((NTG % 2 == 0) ? 2 : 3)));
+    constexpr int PD = R == 2 ? 1 : 2;   // B prefetch distance in steps
+    // chunks per loop trip: the smallest KU with KU * NTG a multiple of R
+    constexpr int KU = (NTG % R == 0) ? 1 : ((2 * NTG) % R == 0 ? 2 : ((3 * NTG) % R == 0 ? 3 : 4));
+    static_assert((KU * NTG) % R == 0, "B ring");
+    u32x4 fb[R][NPB][TN];
+    // the pack's step index of the group's step tl (compile-time) of chunk k (tl may run past the chunk)
+    auto gstep = [&](int k, int tl) { return (k + tl / NTG) * NTAPS + T0 + tl % NTG; };
+#pragma unroll
+    for (int q = 0; q < PD; ++q) load_b(gstep(0, q), fb[q]);
+    __syncthreads();
+
+    // one chunk; KSI = chunk index mod KU (compile-time), so the group's step (k, tl) sits in ring slot
+    // (KSI*NTG + tl) % R.  During chunk k, step tl also splits halo quads [tl*QPS, (tl+1)*QPS) of chunk
+    // k+1 (in the registers since chunk k-1) into the other plane set -- free since the barrier that
+    // ended chunk k-1 -- and refills those registers with chunk k+2: the split's VALU work and its LDS
+    // stores sit between this wave's MFMAs instead of in a serial phase before the barrier.
+    constexpr int QPS = (NQ + NTG - 1) / NTG;
+    // PAR: chunks unrolled in pairs so that a chunk's parity (its plane set, the next chunk's sign) is
+    // a compile-time constant: the sign folds into the split's instructions, the set into LDS offsets
+    constexpr bool PAR = FIX && KU == 1 && NTG <= 9 && TW == 8;   // (16-wide: the pair spills)
+    auto chunk = [&](int k, auto ks, auto kpar) {
+      constexpr int KSI = decltype(ks)::value;
+      constexpr int KP = decltype(kpar)::value;   // k & 1 when >= 0
+      const int kodd = KP >= 0 ? KP : (k & 1);
+      const char* set = smem + kodd * SET;
+      char* nset = smem + (kodd ^ 1) * SET;
+      const float nsg = WD_ALT ? (kodd ? 1.f : -1.f) : 1.f;   // sign of chunk k + 1
+      const int kn = k + 2 < nchunks ? k + 2 : nchunks - 1;
 #if WD_ALT
-    if (k > 0)   // exact sign flip: the running sum changes sign with the chunk's parts
+      if (k > 0)   // exact sign flip: the running sum changes sign with the chunk's parts
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = -acc[i][j];
+          for (int j = 0; j < TN; ++j) acc[i][j] = -acc[i][j];
 #endif
-    int toff = FIX ? 0 : p.toff0, cx = 0;   // tap grid cursor (scalar; FIX: the tap index)
-    if constexpr (FIX) {
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) ab[sp][i] = abase[sp][i] + kodd * SET;
-    } else {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        hb[i] = hbase[i];
-        asm volatile("" : "+v"(hb[i]));
-      }
-    }
-#pragma unroll
-    for (int pl = 0; pl < NPA; ++pl) load_a_part(set, toff, pl, fa);
-#pragma unroll
-    for (int t = 0; t < NTAPS; ++t) {
-      const int sr = KS * NTAPS + t;
-      // kept in this order by the scheduling barriers: the prefetches are issued before this
-      // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
-#if !(WD_ABL & 2)
-      load_b(k * NTAPS + t + PD, fb[(sr + PD) % R]);
-#endif
+      int toff = FIX ? T0 : p.toff0, cx = 0;   // tap grid cursor (scalar; FIX: the tap index)
       if constexpr (FIX) {
-        toff = t + 1;
-      } else if (t + 1 < NTAPS) {
-        toff += p.xstep;
-        if (++cx == p.nx) {
-          cx = 0;
-          toff += p.ystep - p.nx * p.xstep;
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) ab[sp][i] = abase[sp][i] + kodd * SET;
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          hb[i] = hbase[i];
+          asm volatile("" : "+v"(hb[i]));
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
-      step(set, toff, t + 1 < NTAPS, fb[sr % R], [&]() {
+#pragma unroll
+      for (int pl = 0; pl < NPA; ++pl) load_a_part(set, toff, pl, fa);
+#pragma unroll
+      for (int tl = 0; tl < NTG; ++tl) {
+        const int sr = KSI * NTG + tl;
+        // kept in this order by the scheduling barriers: the prefetches are issued before this
+        // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
+#if !(WD_ABL & 2)
+        load_b(gstep(k, tl + PD), fb[(sr + PD) % R]);
+#endif
+        if constexpr (FIX) {
+          toff = T0 + tl + 1;
+        } else if (tl + 1 < NTG) {
+          toff += p.xstep;
+          if (++cx == p.nx) {
+            cx = 0;
+            toff += p.ystep - p.nx * p.xstep;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        step(set, toff, tl + 1 < NTG, fb[sr % R], [&]() {
 #if !(WD_ABL & 1)
 #pragma unroll
-        for (int i = t * QPS; i < (t + 1) * QPS && i < NQ; ++i) {
-          split_quad(i, nsg, nset);
+          for (int i = tl * QPS; i < (tl + 1) * QPS && i < NQ; ++i) {
+            split_quad(i, nsg, nset);
 #if WD_ABL & 32   // diagnostic: always chunk 0 (L2-resident): separates HBM latency from the split work
-          load_quad(i, 0);
+            load_quad(i, 0);
 #else
-          load_quad(i, kn);
+            load_quad(i, kn);
 #endif
-        }
+          }
 #endif
-      });
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-  };
-  using NOPAR = std::integral_constant<int, -1>;
-  if constexpr (PAR) {
-    for (int k = 0; k < nchunks; k += 2) {
-      chunk(k, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-      if (k + 1 >= nchunks) break;
-      chunk(k + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-    }
-  } else {
-    for (int k = 0; k < nchunks; k += KU) {
-      chunk(k, std::integral_constant<int, 0>{}, NOPAR{});
-      if constexpr (KU >= 2) {
+        });
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();
+    };
+    using NOPAR = std::integral_constant<int, -1>;
+    if constexpr (PAR) {
+      for (int k = 0; k < nchunks; k += 2) {
+        chunk(k, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
         if (k + 1 >= nchunks) break;
-        chunk(k + 1, std::integral_constant<int, 1>{}, NOPAR{});
+        chunk(k + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
       }
-      if constexpr (KU >= 3) {
-        if (k + 2 >= nchunks) break;
-        chunk(k + 2, std::integral_constant<int, 2>{}, NOPAR{});
-      }
-      if constexpr (KU >= 4) {
-        if (k + 3 >= nchunks) break;
-        chunk(k + 3, std::integral_constant<int, 3>{}, NOPAR{});
+    } else {
+      for (int k = 0; k < nchunks; k += KU) {
+        chunk(k, std::integral_constant<int, 0>{}, NOPAR{});
+        if constexpr (KU >= 2) {
+          if (k + 1 >= nchunks) break;
+          chunk(k + 1, std::integral_constant<int, 1>{}, NOPAR{});
+        }
+        if constexpr (KU >= 3) {
+          if (k + 2 >= nchunks) break;
+          chunk(k + 2, std::integral_constant<int, 2>{}, NOPAR{});
+        }
+        if constexpr (KU >= 4) {
+          if (k + 3 >= nchunks) break;
+          chunk(k + 3, std::integral_constant<int, 3>{}, NOPAR{});
+        }
       }
     }
+  };
+  if constexpr (KS == 1) {
+    run_group(std::integral_constant<int, 0>{});
+  } else {
+    // (both groups pass the same barriers: one before the loop, one per chunk)
+    if (kg == 0) run_group(std::integral_constant<int, 0>{});
+    else run_group(std::integral_constant<int, 1>{});
   }
 
   // with WD_ALT an even chunk count leaves the running sum negated
   const float oscale = (WD_ALT && nchunks > 0 && !(nchunks & 1)) ? -SM::scale : SM::scale;
   constexpr int CTS = 32 * 33;
+  if constexpr (KS > 1) {
+    // tap group 1 hands its sums to group 0 (the plane sets are free after the last chunk's barrier;
+    // the hand-over area lies past group 0's epilogue staging)
+    float* red = (float*)smem + (WM * WN) * (EPI_ALL ? TM * TN : 1) * CTS + wl * (TM * TN * 16 * 64);
+    if (kg == 1) {
+#pragma unroll
+      for (int qq = 0; qq < TM * TN; ++qq)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(qq * 16 + r) * 64 + lane] = acc[qq / TN][qq % TN][r];
+    }
+    __syncthreads();
+    if (kg == 1) return;
+#pragma unroll
+    for (int qq = 0; qq < TM * TN; ++qq)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[qq / TN][qq % TN][r] += red[(qq * 16 + r) * 64 + lane];
+  }
   if constexpr (EPI_ALL) {
     // every accumulator tile of the wave is staged in LDS first (the plane sets are free after the
     // last barrier): the accumulators are dead before the epilogue loads its operands
-    float* ct = (float*)smem + wave * (TM * TN * CTS);
+    float* ct = (float*)smem + wl * (TM * TN * CTS);
 #pragma unroll
     for (int qq = 0; qq < TM * TN; ++qq)
 #pragma unroll
@@ -465,7 +509,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 
     epilogue_all<float, TM * TN, TN, decltype(stage), CTS>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN,
                                                             lane, stage);
   } else {
-    float* ct = (float*)smem + wave * CTS;
+    float* ct = (float*)smem + wl * CTS;
     epilogue_all<float, TM * TN, TN>(a, ct, rowpix + wm * WTM, n0 + wn * WTN, sbias + wn * WTN, lane, [&](int q) {
 #pragma unroll
       for (int qq = 0; qq < TM * TN; ++qq)
@@ -479,9 +523,9 @@ __global__ __launch_bounds__(WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM == 32 
 }
 
 template <int MODE, int NTAPS, int TH, int TW, int BN, int WM, int WN, int NQ, int VT = 0, int GEO = 0, int KXT = 0,
-          int OCC = 0, int RF = 0>
+          int OCC = 0, int RF = 0, int KS = 1>
 static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
-  constexpr int NT = WM * WN * 64;
+  constexpr int NT = KS * WM * WN * 64;
   constexpr int NPA = SplitMode<MODE>::NPA;
   if (a.ntaps != (VT > 0 ? 1 : NTAPS) || a.copad % 32 || a.cpad % (16 * (VT > 0 ? VT : 1)) || a.ci % 4 || a.ldx % 4 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt_split % 16))
     return 0;
@@ -548,7 +592,8 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   p.nchunks = a.cpad / (16 * (VT > 0 ? VT : 1));
   const int tail = TH * TW * 4 + BN * 4;
   constexpr int TQ = (TH * TW / WM / 32) * (BN / WN / 32);   // accumulator tiles per wave
-  const int epi_bytes = (NT / 64) * (TQ <= 4 ? TQ : 1) * 32 * 33 * 4;
+  // epilogue staging of the (group-0) waves, plus the tap groups' hand-over area
+  const int epi_bytes = (WM * WN) * (TQ <= 4 ? TQ : 1) * 32 * 33 * 4 + (KS > 1 ? WM * WN * TQ * 16 * 64 * 4 : 0);
   // LDS plan: two plane sets when two workgroups still fit a CU, else one set at two per CU,
   // else the single-workgroup plans
   auto need = [&](int sets) { return (sets * p.set_bytes > epi_bytes ? sets * p.set_bytes : epi_bytes) + tail; };
@@ -566,7 +611,7 @@ static int try_split_wd(const lic_conv_args& a, hipStream_t s, int& status) {
   }();
   p.ncb = (remap_on && ncb > 1 && blocks % 8 == 0) ? ncb : 0;
   dim3 grid = p.ncb ? dim3((unsigned)(blocks * ncb), 1) : dim3((unsigned)blocks, ncb);
-  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT, GEO, KXT, OCC, RF>;
+  auto kern = conv_split_wd_kernel<MODE, NTAPS, TH, TW, BN, WM, WN, NQ, VT, GEO, KXT, OCC, RF, KS>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, 160 * 1024);
   if (ea != hipSuccess) {
     status = fail(std::string("split wd conv: dynamic LDS attribute: ") + hipGetErrorString(ea));

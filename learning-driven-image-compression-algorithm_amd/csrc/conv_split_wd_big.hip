@@ -5,16 +5,17 @@
 namespace lic {
 
 int wd_dispatch_big(const lic_conv_args& a, hipStream_t s, int& status) {
-  // experiment switch (LIC_WD_BN192=1: 16x16 px x 192 ch on 8 waves; =2: on 4 waves, one per SIMD)
-  const int bn192 = wd_env("LIC_WD_BN192", 0);
+  // 192 output channels per workgroup (8 waves, 4 x 2, two 32x32 x three accumulator tiles each): the
+  // halo of a tile is read and split once instead of once per 64-channel block (3x3 @64^2 376.6 ->
+  // 360.4 us; profiles/r04/wd_ab.txt).  A/B: LIC_WD_BN192=0 (64-channel blocks)
+  const int bn192 = wd_env("LIC_WD_BN192", 1);
   auto blocks = [&](int th, int tw, int bn) {
     return (int64_t)a.n * ((a.mi + th - 1) / th) * ((a.mj + tw - 1) / tw) * (a.copad / bn);
   };
   if (!(a.mi > 8 && a.mj > 8 && blocks(16, 16, 64) >= 256)) return 0;
   switch (a.ntaps) {
     case 9:   // 3x3 grids (stride 1, stride-2 phases, ConvT phases): compile-time addressing (GEO 1), else general
-      if (bn192 == 1 && a.copad == 192 && try_split_wd<2, 9, 16, 16, 192, 4, 2, 3, 0, 1, 0, 2, 2>(a, s, status)) return 1;
-      if (bn192 == 2 && a.copad == 192 && try_split_wd<2, 9, 16, 16, 192, 2, 2, 6, 0, 1, 0, 1, 3>(a, s, status)) return 1;
+      if (bn192 && a.copad == 192 && try_split_wd<2, 9, 16, 16, 192, 4, 2, 3, 0, 1, 0, 2, 2>(a, s, status)) return 1;
       if (try_split_wd<2, 9, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status)) return 1;
       return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);
     case 6:   // 3x2 / 2x3 phases (ConvT, stride-2)

@@ -27,6 +27,12 @@ int wd_dispatch_small(const lic_conv_args& a, hipStream_t s, int& status) {
     if (a.ntaps == 1 && a.cpad % 32 == 0 && small1x1)
       return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
     if (a.ntaps == 9) {
+      // fewer workgroups than the GPU holds (the slice loop's cc / LRP transforms, B x 4 tiles x a few
+      // channel blocks): two tap groups of 4 waves per workgroup, half the dependent chain per wave.
+      // A/B: LIC_WD_TAPSPLIT=0
+      if (wd_env("LIC_WD_TAPSPLIT", 1) && blocks(8, 8, 64) <= 512 &&
+          try_split_wd<2, 9, 8, 8, 64, 2, 2, 1, 0, 1, 0, 0, 0, 2>(a, s, status))
+        return 1;
       if (try_split_wd<2, 9, 8, 8, 64, 2, 2, 2, 0, 1>(a, s, status)) return 1;
       return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);
     }

@@ -161,9 +161,10 @@ def _cpad_for(ci: int, dtype: torch.dtype) -> int:
 
 
 def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad, dtype: torch.dtype,
-                groups: int = 1, cin_to: Optional[int] = None) -> ConvPack:
+                groups: int = 1, cin_to: Optional[int] = None, cpad_to: Optional[int] = None) -> ConvPack:
     """nn.Conv2d weight [co, ci/g, kh, kw] -> packed [copad][kh*kw][cpad]; pad = (top, left, bottom, right).
-    cin_to: treat the input as cin_to channels (extra channels known zero; zero weights)."""
+    cin_to: treat the input as cin_to channels (extra channels known zero; zero weights).
+    cpad_to: an explicit packed channel count (>= cin; e.g. one 8-channel fp32 halo chunk)."""
     co, cig, kh, kw = weight.shape
     pt, pl, pb, pr = pad
     cin = cig if cin_to is None else cin_to
@@ -171,6 +172,15 @@ def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
     # grouped) go to the direct kernel, which wants the weights unpadded
     epc = 8 if dtype != torch.float32 else 4
     cpad = _cpad_for(cin, dtype) if (groups == 1 and cin % epc == 0) else cin
+    if dtype == torch.float32 and kh * kw == 1 and groups == 1 and cpad % 32 == 16:
+        # fp32 1x1 with an odd number of 16-channel chunks (the slice loop's in_conv, 240 / 336 -> 128):
+        # one zero chunk more lets the fp32x6 virtual-tap tiles (two chunks per barrier) take it
+        # instead of the register GEMM (40 -> ~12 us in the slice loop); zero on both sides
+        cpad += 16
+    if cpad_to is not None:
+        if cpad_to < cin or groups != 1:
+            raise ValueError("pack_conv2d: cpad_to below the channel count or grouped")
+        cpad = cpad_to
     copad = _choose_copad(co)
     # one permute+cast copy kernel (plus a fill when padded): the training path re-packs
     # every conv each step, so launches count

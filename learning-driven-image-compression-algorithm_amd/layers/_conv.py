@@ -44,12 +44,12 @@ class Conv2d(nn.Conv2d, _PackCache):
     """nn.Conv2d (square kernel, symmetric padding) executed by lic_conv2d_fwd."""
 
     def packed(self, dtype: torch.dtype, pad: Optional[Tuple[int, int, int, int]] = None,
-               cin_to: Optional[int] = None) -> Fn.ConvPack:
+               cin_to: Optional[int] = None, cpad_to: Optional[int] = None) -> Fn.ConvPack:
         if pad is None:
             p = self.padding[0]
             pad = (p, p, p, p)
-        return self._get_pack((dtype, pad, cin_to), lambda: Fn.pack_conv2d(
-            self.weight, self.bias, self.stride[0], pad, dtype, self.groups, cin_to))
+        return self._get_pack((dtype, pad, cin_to, cpad_to), lambda: Fn.pack_conv2d(
+            self.weight, self.bias, self.stride[0], pad, dtype, self.groups, cin_to, cpad_to))
 
     def run(self, x: Act, out: Optional[Act] = None, *, pad=None, act: int = ACT_NONE, slope: float = 0.01,
             epi: int = EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
@@ -75,7 +75,12 @@ class Conv2d(nn.Conv2d, _PackCache):
         if self.groups == 1 and x.c % epc and x.zpad >= -(-x.c // epc) * epc and x.c == self.in_channels:
             # zero-padded small-channel input (e.g. the 3-channel image): run as Cin = 16 B on MFMA
             cp = -(-x.c // epc) * epc
-            pk = self.packed(x.dtype, pad, cin_to=cp)
+            # fp32 (the image's 3 channels, exact-fp32 halo kernel): ONE 8-channel chunk instead of the
+            # 16 the packs default to -- the second chunk was all zeros on both sides, so the result is
+            # bit-identical at half the MFMA work
+            # (k x k only: the 1x1 skip keeps its 16-channel pack and kernels)
+            cpad8 = 8 if (x.dtype == torch.float32 and cp <= 8 and k > 1) else None
+            pk = self.packed(x.dtype, pad, cin_to=cp, cpad_to=cpad8)
             return Fn.conv(Act(x.t, x.c0, cp), pk, out, act=act, slope=slope, epi=epi, r1=r1, g=g, r2=r2, y2=y2,
                            prologue=prologue, shuffle=shuffle)
         pk = self.packed(x.dtype, pad)

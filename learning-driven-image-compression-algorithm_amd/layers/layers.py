@@ -50,7 +50,8 @@ class Win_noShift_Attention(nn.Module):
 
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
         side = None
-        if x.B * x.H * x.W <= self.CONCURRENT_MAX_PIX and "wnsa" not in os.environ.get("LIC_DEBUG_SERIAL", ""):
+        if (x.B * x.H * x.W <= self.CONCURRENT_MAX_PIX and os.environ.get("LIC_CONCURRENT_RU", "0") == "1" and
+                "wnsa" not in os.environ.get("LIC_DEBUG_SERIAL", "")):
             ss = self.__dict__.setdefault("_lic_streams", {})
             if str(x.t.device) not in ss:
                 ss[str(x.t.device)] = torch.cuda.Stream(device=x.t.device)

@@ -130,8 +130,9 @@ class SWAtten(AttentionBlock):
             self.out_conv = conv1x1(inter_dim, output_dim)
 
     def _side(self, device):
-        """The stream conv_a runs on (None: serial, LIC_DEBUG_SERIAL containing 'swatten')."""
-        if "swatten" in os.environ.get("LIC_DEBUG_SERIAL", ""):
+        """The stream conv_a runs on (None: serial unless LIC_CONCURRENT_RU=1, or LIC_DEBUG_SERIAL
+        containing 'swatten')."""
+        if os.environ.get("LIC_CONCURRENT_RU", "0") != "1" or "swatten" in os.environ.get("LIC_DEBUG_SERIAL", ""):
             return None
         ss = self.__dict__.setdefault("_lic_streams", {})
         if str(device) not in ss:

@@ -146,17 +146,19 @@ def test_split_net_parity(arch, B, precision):
 
 
 @pytest.mark.parametrize("mode", [2])
-def test_split_conv_transpose_phases(mode):
-    """s_model's ZeroPad2d((1,0,1,0)) + ConvTranspose2d(5, 2, 3, op=1), 192 -> 192, 32^2 -> 64^2 at
+@pytest.mark.parametrize("S", [32, 16])
+def test_split_conv_transpose_phases(mode, S):
+    """s_model's ZeroPad2d((1,0,1,0)) + ConvTranspose2d(5, 2, 3, op=1), 192 -> 192, S^2 -> (2S)^2 at
     B=32: its four sub-pixel phase convolutions (9, 6, 6 and 4 taps) on the weights-direct split
-    kernel, against torch fp32 on the CPU and the exact-fp32 MFMA kernel."""
+    kernel (16x16-px tiles at S = 32, 8x8-px tiles at S = 16), against torch fp32 on the CPU and the
+    exact-fp32 MFMA kernel."""
     import lic_amd.functional as Fn
     from lic_amd.layers import ConvTranspose2d
     torch.manual_seed(61)
     m = ConvTranspose2d(192, 192, 5, 2, 3, output_padding=1).to(DEV)
     with torch.no_grad():
         m.bias.normal_(0, 0.1)
-    x = torch.randn(32, 192, 32, 32) * 0.5
+    x = torch.randn(32, 192, S, S) * 0.5
     X = Fn.Act.from_nchw(x.to(DEV).contiguous(), torch.float32)
     exact = m.run(X, prepad=(1, 1)).nchw().cpu()
     with Fn.split_f32(mode):
@@ -164,7 +166,7 @@ def test_split_conv_transpose_phases(mode):
     ref = F.conv_transpose2d(F.pad(x, (1, 0, 1, 0)), m.weight.detach().cpu(), m.bias.detach().cpu(), 2, 3, 1)
     scale = ref.abs().max().item()
     err, err0 = (got - ref).abs().max().item(), (got - exact).abs().max().item()
-    print(f"\n[split{mode} convT5x5 s2 B=32 32^2] max err vs torch {err:.2e}, vs exact kernel {err0:.2e} (scale {scale:.2f})")
+    print(f"\n[split{mode} convT5x5 s2 B=32 {S}^2] max err vs torch {err:.2e}, vs exact kernel {err0:.2e} (scale {scale:.2f})")
     assert not torch.equal(got, exact)
     assert err <= 3e-6 * scale and err0 <= 5e-6 * scale
 
@@ -198,3 +200,29 @@ def test_split_patch_path_first_conv(k, s, act, monkeypatch):
     assert not torch.equal(got, exact)          # the patch path ran (a different summation order)
     assert (got.double() - base).abs().max().item() <= 3e-6 * scale
     assert (got - exact).abs().max().item() <= 5e-6 * scale
+
+
+@pytest.mark.parametrize("split", [0, 2])
+def test_first_conv_one_fp32_chunk_is_bit_identical(split):
+    """The image's 3x3 s2 conv (3 channels, zero-padded pixels) packs ONE 8-channel fp32 chunk
+    (layers/_conv.py cpad_to=8): bit-identical to the 16-channel pack it replaced (whose second chunk
+    was zeros on both sides), on the exact path and with fp32x6 on (it stays on the exact kernel)."""
+    import lic_amd.functional as Fn
+    from lic_amd import _ffi as L
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(3)
+    m = Conv2d(3, 192, 3, 2, 1).to(DEV)
+    with torch.no_grad():
+        m.bias.normal_(0, 0.1)
+    x = torch.rand(8, 3, 256, 256) * 2 - 1
+    X = Fn.Act.from_nchw(x.to(DEV), torch.float32, pad16=True)
+    with Fn.split_f32(split):
+        got = m.run(X, act=L.ACT_LRELU).nchw().cpu()
+        pk16 = m.packed(torch.float32, None, cin_to=4)
+        assert pk16.cpad == 16
+        ref = Fn.conv(Fn.Act(X.t, X.c0, 4), pk16, act=L.ACT_LRELU).nchw().cpu()
+    assert m.packed(torch.float32, None, cin_to=4, cpad_to=8).cpad == 8
+    assert torch.equal(got, ref)
+    base = F.leaky_relu(F.conv2d(x.double(), m.weight.detach().cpu().double(), m.bias.detach().cpu().double(), 2, 1),
+                        0.01)
+    assert (got.double() - base).abs().max().item() <= 1e-6 * base.abs().max().item()
