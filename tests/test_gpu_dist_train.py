@@ -91,11 +91,16 @@ def _graph_worker(port, q):
     all-reduce (force=True runs the collective path at world 1) eager, and the same step captured
     in a hipGraph (train_net_unet.py --graph at world > 1) and replayed."""
     import copy
+    import sys
     import torch.distributed as dist
+
+    def say(msg):   # progress on stderr (a hang is located by the last line)
+        print(f"[graph worker] {msg}", file=sys.stderr, flush=True)
     from lic_amd import distributed as D
     from lic_amd.model import net_ga, net_unet_ha_hs
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    say("process group up")
     torch.manual_seed(0)
     base = net_ga.synthetic_syntax_bias_(net_unet_ha_hs.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False,
                                                             precision="bf16"))
@@ -124,6 +129,7 @@ def _graph_worker(port, q):
     for _ in range(steps):
         oa.zero_grad(set_to_none=True)
         losses_a.append(body(net_a, pa, oa, sa_, ta).item())
+        say(f"eager step {len(losses_a)}: loss {losses_a[-1]:.6f}")
     launched = len(sa_.buckets)
     net_b, pb, ob, sb_, tb = make()
     side = torch.cuda.Stream()
@@ -132,14 +138,19 @@ def _graph_worker(port, q):
         ob.zero_grad(set_to_none=True)
         first = body(net_b, pb, ob, sb_, tb).item()
     torch.cuda.current_stream().wait_stream(side)
+    say("warm-up step on the capture stream done")
     ob.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=side):
+    # as train_net_unet.py: thread_local capture (the process group's watchdog thread polls events)
+    with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
         out = body(net_b, pb, ob, sb_, tb)
+    say("captured")
     losses_b = [first]
     for _ in range(steps - 1):
         g.replay()
         losses_b.append(out.item())
+        say(f"replay {len(losses_b) - 1}: loss {losses_b[-1]:.6f}")
     torch.cuda.synchronize()
     d = max(((p - q).norm() / (p.norm() + 1e-12)).item() for p, q in zip(net_a.parameters(), net_b.parameters()))
     q.put((losses_a, losses_b, d, launched))
@@ -155,8 +166,13 @@ def test_graph_step_with_rccl_allreduce_matches_eager():
     q = ctx.Queue()
     p = ctx.Process(target=_graph_worker, args=(_free_port(), q))
     p.start()
-    losses_a, losses_b, d, nb = q.get(timeout=300)
-    p.join(timeout=60)
+    try:   # bounded: a hung collective fails the test instead of stalling the suite
+        losses_a, losses_b, d, nb = q.get(timeout=150)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+            p.join()
     print(f"\n[graph + RCCL all-reduce, {nb} buckets] eager losses {losses_a}, graph losses {losses_b}, "
           f"max relative parameter difference {d:.2e}")
     assert p.exitcode == 0

@@ -153,8 +153,11 @@ def main():
                 seed_t.add_(1)
         torch.cuda.current_stream().wait_stream(side)
         opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize(dev)   # the warm-up's collectives complete before the capture starts
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=side):   # the warm-up's stream: AccumulateGrad nodes stay on it
+        # the warm-up's stream: AccumulateGrad nodes stay on it.  thread_local: RCCL's watchdog thread
+        # keeps querying its events during the capture (a global-mode capture makes that an error)
+        with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
             outs = step_body(static_x, seed_t)
             seed_t.add_(1)
 
