@@ -506,15 +506,33 @@ typedef struct lic_resunit_args {
 } lic_resunit_args;
 int lic_resunit_fwd(const lic_resunit_args* a, lic_stream_t stream);
 
+/* fp32x6 WinBasedAttention core in one launch (abi 6): qkv Linear + the shifted-window attention of
+ * lic_win_attn_fwd (WBA: q*scale before the dot, mask_kind 1) without the qkv map in HBM, for
+ * C = 192, 8 heads, 8x8 windows (the Win_noShift_Attention blocks at 64x64, layers/layers.py:87-102;
+ * layers/win_attention.py:85-116,154-209).  out = the attention output (C channels per pixel) that
+ * the proj Linear consumes; bit-identical to lic_conv2d_fwd(qkv, mfma_mode 2) + lic_win_attn_fwd
+ * (mfma_mode 2).  qkv_wsplit = the fp32x6 split pack of the qkv weights in MFMA-fragment order
+ * ([18][12][1][3][64][8] bf16), qkv_bias [576] fp32. */
+typedef struct lic_wba_args {
+  const float* x; int32_t n, h, w, c, ldx;   /* fp32 NHWC input (the block's x), c = 192 */
+  float* out; int32_t ldo;                   /* fp32 NHWC attention output, c channels */
+  int32_t heads, ws, shift, mask_kind;       /* 8, 8, shift, 1 */
+  float scale;                               /* head_dim ** -0.5 */
+  const float* table; int32_t tab_sr, tab_sh;
+  const void* qkv_wsplit;
+  const float* qkv_bias;
+} lic_wba_args;
+int lic_wba_qkv_attn_fwd(const lic_wba_args* a, lic_stream_t stream);
+
 /* Library info.
  * LIC_ABI_VERSION changes whenever an entry point's parameter list or an args struct's layout
  * changes (3: lic_conv_args.mfma_mode / wgt_split, lic_rate_train_* seed_dev / seed_mul; 5:
- * lic_resunit_args / lic_resunit_fwd).  A
+ * lic_resunit_args / lic_resunit_fwd; 6: lic_wba_args / lic_wba_qkv_attn_fwd).  A
  * caller compiled against this header checks lic_abi_version() == LIC_ABI_VERSION and
  * lic_args_size(k) == sizeof(...) once after loading the library (the Python host does, _ffi.load). */
-#define LIC_ABI_VERSION 5
+#define LIC_ABI_VERSION 6
 enum { LIC_ARGS_CONV = 0, LIC_ARGS_ATTN = 1, LIC_ARGS_RATE = 2, LIC_ARGS_RANS = 3, LIC_ARGS_WGRAD = 4,
-       LIC_ARGS_RESUNIT = 5 };
+       LIC_ARGS_RESUNIT = 5, LIC_ARGS_WBA = 6 };
 const char* lic_last_error(void);
 const char* lic_version(void);          /* "liblic <ver> gfx950 (abi N, src <source hash>)" */
 /* Build provenance: the first 16 hex digits of the SHA-256 of the sources the library was built

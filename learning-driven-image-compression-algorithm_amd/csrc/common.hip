@@ -46,6 +46,7 @@ extern "C" int64_t lic_args_size(int32_t which) {
     case LIC_ARGS_RANS: return (int64_t)sizeof(lic_rans_args);
     case LIC_ARGS_WGRAD: return (int64_t)sizeof(lic_wgrad_args);
     case LIC_ARGS_RESUNIT: return (int64_t)sizeof(lic_resunit_args);
+    case LIC_ARGS_WBA: return (int64_t)sizeof(lic_wba_args);
     default: return -1;
   }
 }

@@ -618,6 +618,39 @@ def win_attn(qkv: Act, C: int, heads: int, ws: int, shift: int, table: torch.Ten
     return out
 
 
+def wba_qkv_attn_ok(x: Act, C: int, heads: int, ws: int) -> bool:
+    """The fused fp32x6 qkv + window-attention launch applies (csrc/wba_split.hip): fp32x6, C = 192,
+    8 heads, 8x8 windows, H and W multiples of 8, 16-byte aligned rows -- and a map on which the
+    unfused qkv 1x1 runs on the virtual-tap split kernel (>= 64 K pixels, W >= 16,
+    csrc/conv_split_wd.hip), whose arithmetic the fused launch reproduces bit for bit: the model's
+    numerics do not depend on whether the fusion runs."""
+    return (split_mode() == 2 and x.dtype == torch.float32 and C == 192 and heads == 8 and ws == 8 and
+            x.c == C and x.H % 8 == 0 and x.W % 8 == 0 and x.W >= 16 and x.B * x.H * x.W >= 65536 and
+            x.ld % 4 == 0 and x.ptr % 16 == 0)
+
+
+def wba_qkv_attn(x: Act, qkv_pk: ConvPack, heads: int, ws: int, shift: int, table: torch.Tensor, tab_sr: int,
+                 tab_sh: int, mask_kind: int, scale: float, out: Optional[Act] = None) -> Act:
+    """lic_wba_qkv_attn_fwd: qkv Linear + shifted-window attention of an fp32 map in one launch
+    (bit-identical to conv(x, qkv_pk) + win_attn(...) under fp32x6); returns the C-channel attention
+    output that the proj Linear consumes."""
+    C = x.c
+    ws2 = split_weights(qkv_pk, 2)
+    if ws2 is None or qkv_pk.copad != 3 * C or qkv_pk.cpad != C or qkv_pk.bias is None:
+        raise _ffi.LicError("wba_qkv_attn: the qkv pack must be an fp32 [3C][1][C] pack with a bias")
+    if out is None:
+        out = Act.empty(x.B, x.H, x.W, C, x.dtype, x.t.device)
+    a = _ffi.WbaArgs()
+    a.x, a.n, a.h, a.w, a.c, a.ldx = x.ptr, x.B, x.H, x.W, C, x.ld
+    a.out, a.ldo = out.ptr, out.ld
+    a.heads, a.ws, a.shift, a.mask_kind = heads, ws, shift, mask_kind
+    a.scale = scale
+    a.table, a.tab_sr, a.tab_sh = _dp(table), tab_sr, tab_sh
+    a.qkv_wsplit, a.qkv_bias = _dp(ws2), _dp(qkv_pk.bias)
+    check(_lib().lic_wba_qkv_attn_fwd(ctypes.byref(a), stream_handle()))
+    return out
+
+
 def layernorm(x: Act, weight: torch.Tensor, bias: torch.Tensor, eps: float, out: Optional[Act] = None) -> Act:
     if out is None:
         out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)

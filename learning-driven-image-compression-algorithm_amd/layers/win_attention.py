@@ -6,6 +6,7 @@ WinBasedAttention.run = qkv Linear (1x1 GEMM, lic_conv2d_fwd)
                          + softmax + AV + reverse + roll back)
                       -> proj Linear with the shortcut add fused in its epilogue.
 """
+import os
 from typing import Optional
 
 import torch
@@ -16,6 +17,8 @@ from ..functional import Act
 from ._conv import Linear
 
 __all__ = ["WindowAttention", "WinBasedAttention", "window_partition", "window_reverse"]
+
+_FUSED = os.environ.get("LIC_FUSED_WBA", "1") != "0"
 
 
 def window_partition(x, window_size=8):
@@ -75,7 +78,15 @@ class WinBasedAttention(nn.Module):
                                     qkv_bias=qkv_bias, qk_scale=qk_scale, attn_drop=attn_drop, proj_drop=drop)
 
     def run(self, x: Act, out: Optional[Act] = None, **proj_kw) -> Act:
-        """out = x + proj(attention(qkv(x))); extra epilogue kwargs go to the proj launch."""
+        """out = x + proj(attention(qkv(x))); extra epilogue kwargs go to the proj launch.  Under fp32x6
+        at C = 192 / 8 heads / 8x8 windows the qkv Linear and the attention are one launch
+        (Fn.wba_qkv_attn: the 3C qkv map never reaches HBM; bit-identical; LIC_FUSED_WBA=0 for the
+        three-launch path)."""
+        if _FUSED and Fn.wba_qkv_attn_ok(x, self.dim, self.num_heads, self.window_size):
+            a = Fn.wba_qkv_attn(x, self.attn.qkv.packed(x.dtype), self.num_heads, self.window_size, self.shift_size,
+                                self.attn.relative_position_bias_table, self.num_heads, 1,
+                                1 if self.shift_size > 0 else 0, float(self.attn.scale))
+            return self.attn.proj.run(a, out, r1=x, **proj_kw)
         qkv = self.attn.qkv.run(x)
         a = Fn.win_attn(qkv, self.dim, self.num_heads, self.window_size, self.shift_size,
                         self.attn.relative_position_bias_table, self.num_heads, 1,

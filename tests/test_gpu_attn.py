@@ -139,3 +139,48 @@ def test_mfma_attention_8_wave_groups(C, heads, shift, mask_kind):
     ref = _attn_ref(qkv.to(torch.float16).float(), C, heads, ws, shift, table, mask_kind, False, scale)
     out = _run(qkv, C, heads, ws, shift, table, mask_kind, False, scale, torch.float16, False)
     assert (out - ref).abs().max().item() <= 1e-2 * (ref.abs().max().item() + 1e-6)
+
+
+@pytest.mark.parametrize("B,H,W,shift", [(16, 64, 64, 4), (32, 64, 64, 2), (8, 128, 64, 0), (32, 64, 64, 4),
+                                         (2, 64, 64, 4), (1, 16, 16, 4), (1, 32, 64, 0)])
+def test_fused_wba_bit_exact(B, H, W, shift):
+    """lic_wba_qkv_attn_fwd (csrc/wba_split.hip: fp32x6 qkv Linear + window attention in one launch)
+    equals the unfused launches (qkv 1x1 on the virtual-tap split kernel + lic_win_attn_fwd, mfma_mode
+    2) bit for bit where the model uses it (>= 64 K pixels: the qkv 1x1 is then a virtual-tap launch),
+    and so does WinBasedAttention.run with and without the fusion; on every map the launch matches the
+    PyTorch float64 restatement at the fp32x6 bar (smaller maps keep the unfused path, whose qkv runs
+    on other split kernels)."""
+    from lic_amd import functional as Fn
+    from lic_amd.functional import Act
+    from lic_amd.layers import win_attention as WA
+    torch.manual_seed(7)
+    m = WA.WinBasedAttention(dim=192, num_heads=8, window_size=8, shift_size=shift).to(DEV)
+    with torch.no_grad():
+        m.attn.relative_position_bias_table.normal_(0.0, 0.5)
+        m.attn.qkv.bias.normal_(0.0, 0.3)
+    x = Act(torch.randn(B, H, W, 192, device=DEV))
+    mk = 1 if shift > 0 else 0
+    sc = float(m.attn.scale)
+    tab = m.attn.relative_position_bias_table
+    big = B * H * W >= 65536
+    with Fn.split_f32(2):
+        assert Fn.wba_qkv_attn_ok(x, 192, 8, 8) == big
+        fused = Fn.wba_qkv_attn(x, m.attn.qkv.packed(torch.float32), 8, 8, shift, tab, 8, 1, mk, sc)
+        qkv = m.attn.qkv.run(x)
+        ref = Fn.win_attn(qkv, 192, 8, 8, shift, tab, 8, 1, mk, False, sc)
+        y_fused = m.run(x)
+        WA._FUSED = False
+        try:
+            y_ref = m.run(x)
+        finally:
+            WA._FUSED = True
+    torch.cuda.synchronize()
+    if big:
+        assert torch.equal(fused.t, ref.t)
+    assert torch.equal(y_fused.t, y_ref.t)
+    # and the op itself against float64 torch on the same weights (fp32x6 grade)
+    w = m.attn.qkv.weight.detach().double().cpu()
+    q64 = x.t.double().cpu() @ w.t() + m.attn.qkv.bias.detach().double().cpu()
+    o64 = _attn_ref(q64, 192, 8, 8, shift, tab.detach().double().cpu(), mk, False, sc)
+    err = (fused.t.double().cpu() - o64).abs().max() / o64.abs().max()
+    assert err < 2e-6, err
