@@ -506,13 +506,14 @@ typedef struct lic_resunit_args {
 } lic_resunit_args;
 int lic_resunit_fwd(const lic_resunit_args* a, lic_stream_t stream);
 
-/* fp32x6 WinBasedAttention core in one launch (abi 6): qkv Linear + the shifted-window attention of
+/* fp32x6 WinBasedAttention in one launch (abi 6): qkv Linear + the shifted-window attention of
  * lic_win_attn_fwd (WBA: q*scale before the dot, mask_kind 1) without the qkv map in HBM, for
  * C = 192, 8 heads, 8x8 windows (the Win_noShift_Attention blocks at 64x64, layers/layers.py:87-102;
- * layers/win_attention.py:85-116,154-209).  out = the attention output (C channels per pixel) that
- * the proj Linear consumes; bit-identical to lic_conv2d_fwd(qkv, mfma_mode 2) + lic_win_attn_fwd
- * (mfma_mode 2).  qkv_wsplit = the fp32x6 split pack of the qkv weights in MFMA-fragment order
- * ([18][12][1][3][64][8] bf16), qkv_bias [576] fp32. */
+ * layers/win_attention.py:85-116,154-209).  proj_wsplit NULL: out = the attention output (C channels
+ * per pixel) that the proj Linear consumes; else out = x + proj(attention) (the whole block, out !=
+ * x).  Bit-identical to lic_conv2d_fwd(qkv, mfma_mode 2) + lic_win_attn_fwd(mfma_mode 2)
+ * (+ lic_conv2d_fwd(proj, r1 = x)).  *_wsplit = fp32x6 split packs in MFMA-fragment order (qkv
+ * [18][12][1][3][64][8], proj [6][12][1][3][64][8] bf16); biases fp32. */
 typedef struct lic_wba_args {
   const float* x; int32_t n, h, w, c, ldx;   /* fp32 NHWC input (the block's x), c = 192 */
   float* out; int32_t ldo;                   /* fp32 NHWC attention output, c channels */
@@ -521,6 +522,8 @@ typedef struct lic_wba_args {
   const float* table; int32_t tab_sr, tab_sh;
   const void* qkv_wsplit;
   const float* qkv_bias;
+  const void* proj_wsplit;                   /* NULL: attention output only */
+  const float* proj_bias;
 } lic_wba_args;
 int lic_wba_qkv_attn_fwd(const lic_wba_args* a, lic_stream_t stream);
 

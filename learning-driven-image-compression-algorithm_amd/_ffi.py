@@ -153,6 +153,8 @@ class WbaArgs(ctypes.Structure):
         ("table", _vp), ("tab_sr", _i32), ("tab_sh", _i32),
         ("qkv_wsplit", _vp),
         ("qkv_bias", _vp),
+        ("proj_wsplit", _vp),
+        ("proj_bias", _vp),
     ]
 
 

@@ -6,14 +6,16 @@
 // Unfused, the qkv 1x1 conv writes a 3C fp32 map (302 MB per call at 64^2 x 32) that the attention
 // kernel reads straight back.  Here one workgroup owns one window: its 64 tokens are split once into
 // three bf16 planes in LDS, the qkv GEMM of a group of 4 heads goes to LDS, the attention of those
-// heads reads it there, and only the attention output (C per token) goes to HBM; the proj Linear (+
-// shortcut) stays a separate launch.
+// heads reads it there; with PROJ the attention output is split into the (then free) planes and the
+// proj Linear + shortcut finish the block in the same launch (out = x + proj(attn)), else the attention
+// output goes to HBM for a separate proj launch.
 //
 // Bit-identical to the unfused fp32x6 path (conv_split_wd VT 1x1 + win_attn_mfma_kernel<float, 4, 1>):
 // every output element sees the same MFMA sequence -- the qkv accumulator runs over the 12 16-channel
 // steps in order with the six part products smallest first, 32-channel chunk k split from (-1)^k x and
 // the running sum negated at each chunk start (conv_split_wd.h WD_ALT), finished as -acc + bias; the
-// attention takes q * scale, K / Q / V / P split by split8_bf16 and the same product order per tile.
+// attention takes q * scale, K / Q / V / P split by split8_bf16 and the same product order per tile; the
+// proj runs the virtual-tap sequence again on the split attention output, then (-acc + bias) + x.
 // tests/test_gpu_attn.py::test_fused_wba_bit_exact checks torch.equal against the unfused launches.
 #include "lic_common.h"
 #include "conv_split.h"
@@ -45,6 +47,7 @@ __device__ __forceinline__ void split8(float4 lo, float4 hi, u32x4 (&out)[3]) {
 // Persistent: a workgroup per CU walks windows blockIdx.x, + gridDim.x, ...; the next window's
 // activations are loaded into registers before the current one's last attention phase (which issues no
 // loads), so their HBM latency hides behind it.
+template <bool PROJ>
 __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args a) {
   using SM = SplitMode<2>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -75,6 +78,7 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
   if ((int)blockIdx.x < nwin) load_x(blockIdx.x);
 
   for (int win = blockIdx.x; win < nwin; win += gridDim.x) {
+    floatx16 Ok0, Ok1;   // PROJ: this wave's attention output of head group 0 / 1 (head 4g + wave/2)
     const int wx = win % nwx, wy = (win / nwx) % nwy;
     // ---- phase A: the window's 64 x 192 fp32 activations -> three bf16 planes; 32-channel chunk k
     // carries the sign (-1)^k of the unfused kernel's chunk k (conv_split_wd.h, WD_ALT).  (The previous
@@ -285,15 +289,107 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
             for (int pr = SM::NPROD - 1; pr >= 0; --pr) O = mfma_k16<bf16_t>(vp[SM::PA[pr]], pp[SM::PB[pr]], O);
           }
         // lane (query i, half lh) holds channels 8q + 4lh + (0..3), q = 0..3 (24 valid)
-        float* op = a.out + (int64_t)pix_of(win, i) * a.ldo + h * WB_D;
+        if constexpr (PROJ) {
+          if (g == 0) Ok0 = O;
+          else Ok1 = O;
+        } else {
+          float* op = a.out + (int64_t)pix_of(win, i) * a.ldo + h * WB_D;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c0 = 8 * q + 4 * lh;
-          if (c0 < WB_D) *(float4*)(op + c0) = make_float4(O[4 * q], O[4 * q + 1], O[4 * q + 2], O[4 * q + 3]);
+          for (int q = 0; q < 4; ++q) {
+            const int c0 = 8 * q + 4 * lh;
+            if (c0 < WB_D) *(float4*)(op + c0) = make_float4(O[4 * q], O[4 * q + 1], O[4 * q + 2], O[4 * q + 3]);
+          }
         }
       }
     }
-    __syncthreads();   // every wave past this window's phase C before the next window's planes / qkv
+    __syncthreads();   // every wave past this window's phase C (and its qkv GEMMs: the planes are free)
+    if constexpr (PROJ) {
+      // ---- phase D: the attention output split into the planes (32-channel chunk k from (-1)^k o), then
+      // the proj Linear as the unfused virtual-tap launch computes it, + bias + x, at the tokens' pixels
+      {
+        const int hl = wave >> 1, ti = wave & 1, i = 32 * ti + lr;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const int c0 = (4 * g + hl) * WB_D + 8 * q + 4 * lh;   // 8q + 4lh < 24: q < 3
+            const floatx16& Og = g ? Ok1 : Ok0;
+            uint2 parts[3];
+            split4<2>(make_float4(Og[4 * q], Og[4 * q + 1], Og[4 * q + 2], Og[4 * q + 3]),
+                      LIC_PRO_NONE, ((c0 >> 5) & 1) ? -1.f : 1.f, parts);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) *(uint2*)(xp + p * WB_PLANE + i * (WB_XS * 2) + c0 * 2) = parts[p];
+          }
+      }
+      __syncthreads();
+      // 2 token tiles x 6 column tiles: waves 0-3 take two (n-tiles w/2 and 4 + w/2), waves 4-7 one, so the
+      // two waves of every SIMD (w, w + 4) hold three tiles together
+      const int mt = wave & 1;
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)a.proj_wsplit, (short)0, (int)(6 * nsteps * 3 * 1024), 0x00020000);
+      auto proj = [&](auto cnt_c) {
+        constexpr int CNT = decltype(cnt_c)::value;
+        int jt[CNT];
+        jt[0] = wave >> 1;
+        if constexpr (CNT > 1) jt[1] = 4 + (wave >> 1);
+        floatx16 acc[CNT];
+#pragma unroll
+        for (int c = 0; c < CNT; ++c)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+        const char* arow = xp + (32 * mt + lr) * (WB_XS * 2) + lh * 16;
+        auto load_b = [&](int st, u32x4(&fb)[3][CNT]) {
+#pragma unroll
+          for (int c = 0; c < CNT; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+              fb[p][c] = __builtin_amdgcn_raw_buffer_load_b128(prs, lane * 16, ((jt[c] * nsteps + st) * 3 + p) * 1024, 0);
+        };
+        u32x4 fb[3][3][CNT], fa[3];
+        load_b(0, fb[0]);
+        load_b(1, fb[1]);
+#pragma unroll
+        for (int st = 0; st < 12; ++st) {
+          if (st + 2 < 12) load_b(st + 2, fb[(st + 2) % 3]);
+          if (st > 0 && (st & 1) == 0)
+#pragma unroll
+            for (int c = 0; c < CNT; ++c) acc[c] = -acc[c];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) fa[p] = *(const u32x4*)(arow + p * WB_PLANE + st * 32);
+#pragma unroll
+          for (int pr = SM::NPROD - 1; pr >= 0; --pr)
+#pragma unroll
+            for (int c = 0; c < CNT; ++c) acc[c] = mfma_k16<bf16_t>(fa[SM::PA[pr]], fb[st % 3][SM::PB[pr]][c], acc[c]);
+        }
+        // (-acc + bias) + x, as the unfused epilogue (ct = acc * -1, + bias, + r1).  Register r holds
+        // token 32 mt + 8 (r >> 2) + 4 lh + (r & 3): window row 4 mt + (r >> 2), column 4 lh + (r & 3)
+        int rowb[4], colx[4];
+        {
+          const int wb = win / (nwx * nwy);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            int py = wy * WB_WS + 4 * mt + k + a.shift, px = wx * WB_WS + 4 * lh + k + a.shift;
+            if (py >= a.h) py -= a.h;
+            if (px >= a.w) px -= a.w;
+            rowb[k] = (wb * a.h + py) * a.w;
+            colx[k] = px;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CNT; ++c) {
+          const int col = 32 * jt[c] + lr;
+          const float bias = a.proj_bias[col];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int64_t px = rowb[r >> 2] + colx[r & 3];
+            a.out[px * a.ldo + col] = (-acc[c][r] + bias) + a.x[px * a.ldx + col];
+          }
+        }
+      };
+      if (wave < 4) proj(std::integral_constant<int, 2>{});
+      else proj(std::integral_constant<int, 1>{});
+    }
+    __syncthreads();   // every wave done with this window before the next window's planes / qkv
   }
 }
 
@@ -306,14 +402,18 @@ extern "C" int lic_wba_qkv_attn_fwd(const lic_wba_args* a, lic_stream_t stream) 
   if (a->c != WB_C || a->heads != WB_HEADS || a->ws != WB_WS || a->h % WB_WS || a->w % WB_WS || a->n < 1 ||
       a->shift < 0 || a->shift >= WB_WS || a->mask_kind < 0 || a->mask_kind > 2)
     return fail("wba: the fused kernel takes C = 192, 8 heads, 8x8 windows, H and W multiples of 8");
-  if (!a->x || !a->out || !a->qkv_wsplit || !a->qkv_bias || !a->table) return fail("wba: null pointer");
+  if (!a->x || !a->out || !a->qkv_wsplit || !a->qkv_bias || !a->table || (a->proj_wsplit && !a->proj_bias))
+    return fail("wba: null pointer");
+  if (a->proj_wsplit && ((uintptr_t)a->proj_wsplit & 15)) return fail("wba: proj pack not 16-byte aligned");
+  if (a->proj_wsplit && (const void*)a->out == (const void*)a->x) return fail("wba: out must not alias x (the shortcut)");
   if (a->ldx < WB_C || a->ldx % 4 || a->ldo < WB_C || a->ldo % 4 || ((uintptr_t)a->x & 15) || ((uintptr_t)a->out & 15) ||
       ((uintptr_t)a->qkv_wsplit & 15))
     return fail("wba: x / out need 16-byte aligned rows (ld a multiple of 4, >= 192)");
   if ((int64_t)a->n * a->h * a->w * (a->ldx > a->ldo ? a->ldx : a->ldo) >= (1LL << 31))
     return fail("wba: map too large for 32-bit pixel offsets");
   hipStream_t s = (hipStream_t)stream;
-  const hipError_t ea = ensure_dyn_lds((const void*)wba_qkv_attn_kernel, WB_LDS);
+  const hipError_t ea = a->proj_wsplit ? ensure_dyn_lds((const void*)wba_qkv_attn_kernel<true>, WB_LDS)
+                                       : ensure_dyn_lds((const void*)wba_qkv_attn_kernel<false>, WB_LDS);
   if (ea != hipSuccess) return fail(std::string("wba: dynamic LDS attribute: ") + hipGetErrorString(ea));
   const int64_t windows = (int64_t)a->n * (a->h / WB_WS) * (a->w / WB_WS);
   static int cus[64] = {0};   // one workgroup per CU (157 KB of LDS each), persistent over the windows
@@ -322,7 +422,8 @@ extern "C" int lic_wba_qkv_attn_fwd(const lic_wba_args* a, lic_stream_t stream) 
   if (cus[dev] <= 0 && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return fail("wba: CU count");
   const int64_t grid = windows < cus[dev] ? windows : cus[dev];
-  hipLaunchKernelGGL(wba_qkv_attn_kernel, dim3((unsigned)grid), dim3(512), WB_LDS, s, *a);
+  if (a->proj_wsplit) hipLaunchKernelGGL(wba_qkv_attn_kernel<true>, dim3((unsigned)grid), dim3(512), WB_LDS, s, *a);
+  else hipLaunchKernelGGL(wba_qkv_attn_kernel<false>, dim3((unsigned)grid), dim3(512), WB_LDS, s, *a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(std::string("wba launch: ") + hipGetErrorString(e));
 }

@@ -630,14 +630,21 @@ def wba_qkv_attn_ok(x: Act, C: int, heads: int, ws: int) -> bool:
 
 
 def wba_qkv_attn(x: Act, qkv_pk: ConvPack, heads: int, ws: int, shift: int, table: torch.Tensor, tab_sr: int,
-                 tab_sh: int, mask_kind: int, scale: float, out: Optional[Act] = None) -> Act:
+                 tab_sh: int, mask_kind: int, scale: float, out: Optional[Act] = None,
+                 proj_pk: Optional[ConvPack] = None) -> Act:
     """lic_wba_qkv_attn_fwd: qkv Linear + shifted-window attention of an fp32 map in one launch
     (bit-identical to conv(x, qkv_pk) + win_attn(...) under fp32x6); returns the C-channel attention
-    output that the proj Linear consumes."""
+    output that the proj Linear consumes -- or, with proj_pk, the whole block x + proj(attention)
+    (bit-identical to conv(attention, proj_pk, r1=x))."""
     C = x.c
     ws2 = split_weights(qkv_pk, 2)
     if ws2 is None or qkv_pk.copad != 3 * C or qkv_pk.cpad != C or qkv_pk.bias is None:
         raise _ffi.LicError("wba_qkv_attn: the qkv pack must be an fp32 [3C][1][C] pack with a bias")
+    wp = None
+    if proj_pk is not None:
+        wp = split_weights(proj_pk, 2)
+        if wp is None or proj_pk.copad != C or proj_pk.cpad != C or proj_pk.bias is None:
+            raise _ffi.LicError("wba_qkv_attn: the proj pack must be an fp32 [C][1][C] pack with a bias")
     if out is None:
         out = Act.empty(x.B, x.H, x.W, C, x.dtype, x.t.device)
     a = _ffi.WbaArgs()
@@ -647,6 +654,8 @@ def wba_qkv_attn(x: Act, qkv_pk: ConvPack, heads: int, ws: int, shift: int, tabl
     a.scale = scale
     a.table, a.tab_sr, a.tab_sh = _dp(table), tab_sr, tab_sh
     a.qkv_wsplit, a.qkv_bias = _dp(ws2), _dp(qkv_pk.bias)
+    if wp is not None:
+        a.proj_wsplit, a.proj_bias = _dp(wp), _dp(proj_pk.bias)
     check(_lib().lic_wba_qkv_attn_fwd(ctypes.byref(a), stream_handle()))
     return out
 

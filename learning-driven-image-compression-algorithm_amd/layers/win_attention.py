@@ -19,6 +19,7 @@ from ._conv import Linear
 __all__ = ["WindowAttention", "WinBasedAttention", "window_partition", "window_reverse"]
 
 _FUSED = os.environ.get("LIC_FUSED_WBA", "1") != "0"
+_FUSED_PROJ = os.environ.get("LIC_FUSED_WBA_PROJ", "0") == "1"
 
 
 def window_partition(x, window_size=8):
@@ -81,12 +82,16 @@ class WinBasedAttention(nn.Module):
         """out = x + proj(attention(qkv(x))); extra epilogue kwargs go to the proj launch.  Under fp32x6
         at C = 192 / 8 heads / 8x8 windows the qkv Linear and the attention are one launch
         (Fn.wba_qkv_attn: the 3C qkv map never reaches HBM; bit-identical; LIC_FUSED_WBA=0 for the
-        three-launch path)."""
+        three-launch path).  LIC_FUSED_WBA_PROJ=1 also folds the proj + shortcut into that launch
+        (bit-identical, but slower today: DESIGN.md section 5)."""
         if _FUSED and Fn.wba_qkv_attn_ok(x, self.dim, self.num_heads, self.window_size):
+            fuse_proj = _FUSED_PROJ and not proj_kw and (out is None or out.t.data_ptr() != x.t.data_ptr())
             a = Fn.wba_qkv_attn(x, self.attn.qkv.packed(x.dtype), self.num_heads, self.window_size, self.shift_size,
                                 self.attn.relative_position_bias_table, self.num_heads, 1,
-                                1 if self.shift_size > 0 else 0, float(self.attn.scale))
-            return self.attn.proj.run(a, out, r1=x, **proj_kw)
+                                1 if self.shift_size > 0 else 0, float(self.attn.scale),
+                                out=out if fuse_proj else None,
+                                proj_pk=self.attn.proj.packed(x.dtype) if fuse_proj else None)
+            return a if fuse_proj else self.attn.proj.run(a, out, r1=x, **proj_kw)
         qkv = self.attn.qkv.run(x)
         a = Fn.win_attn(qkv, self.dim, self.num_heads, self.window_size, self.shift_size,
                         self.attn.relative_position_bias_table, self.num_heads, 1,

@@ -169,6 +169,10 @@ def test_fused_wba_bit_exact(B, H, W, shift):
         qkv = m.attn.qkv.run(x)
         ref = Fn.win_attn(qkv, 192, 8, 8, shift, tab, 8, 1, mk, False, sc)
         y_fused = m.run(x)
+        # the whole block in the one launch (proj + shortcut fused; opt-in LIC_FUSED_WBA_PROJ=1)
+        y_proj = Fn.wba_qkv_attn(x, m.attn.qkv.packed(torch.float32), 8, 8, shift, tab, 8, 1, mk, sc,
+                                 proj_pk=m.attn.proj.packed(torch.float32))
+        y_proj_ref = m.attn.proj.run(fused, r1=x)
         WA._FUSED = False
         try:
             y_ref = m.run(x)
@@ -178,6 +182,7 @@ def test_fused_wba_bit_exact(B, H, W, shift):
     if big:
         assert torch.equal(fused.t, ref.t)
     assert torch.equal(y_fused.t, y_ref.t)
+    assert torch.equal(y_proj.t, y_proj_ref.t)
     # and the op itself against float64 torch on the same weights (fp32x6 grade)
     w = m.attn.qkv.weight.detach().double().cpu()
     q64 = x.t.double().cpu() @ w.t() + m.attn.qkv.bias.detach().double().cpu()
