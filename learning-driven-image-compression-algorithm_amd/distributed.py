@@ -144,7 +144,13 @@ class GradAllReduce:
     joined through events, wait, scale, scatter), so a training step that calls ``finish()``
     inside ``torch.cuda.graph`` captures the collectives too: replays run the bucketed all-reduce
     with no host work (train_net_unet.py --graph at world > 1).  ``force`` runs the collective
-    path at world 1 as well (a one-rank all-reduce: the graph-capture test of the path)."""
+    path at world 1 as well (a one-rank all-reduce: the graph-capture test of the path).
+
+    ``defer = True`` (set around a hipGraph capture) launches every bucket from ``finish()`` on the
+    capturing thread instead of from the backward's hooks: a collective issued from the autograd
+    thread is queued to the process group's watchdog, whose event queries then fail on events
+    recorded in a capturing stream (hipErrorCapturedEvent, seen on MI355X).  The replays run the
+    same collectives with no host work either way."""
 
     def __init__(self, params, world: int, bucket_mb: float = 32.0, force: bool = False):
         self.world = world
@@ -166,6 +172,7 @@ class GradAllReduce:
         self._flat = [None] * len(buckets)
         self._members = [None] * len(buckets)
         self._hooks = []
+        self.defer = False
         if self.active:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -173,7 +180,7 @@ class GradAllReduce:
     def _on_grad(self, p):
         i = self._where[id(p)]
         self._pending[i] -= 1
-        if self._pending[i] == 0:
+        if self._pending[i] == 0 and not self.defer:
             self._launch(i)
 
     def _launch(self, i):

@@ -141,6 +141,7 @@ def _graph_worker(port, q):
     say("warm-up step on the capture stream done")
     ob.zero_grad(set_to_none=True)
     torch.cuda.synchronize()
+    sb_.defer = True   # collectives launched from finish() on this (capturing) thread
     g = torch.cuda.CUDAGraph()
     # as train_net_unet.py: thread_local capture (the process group's watchdog thread polls events)
     with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):

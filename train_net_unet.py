@@ -154,6 +154,7 @@ def main():
         torch.cuda.current_stream().wait_stream(side)
         opt.zero_grad(set_to_none=True)
         torch.cuda.synchronize(dev)   # the warm-up's collectives complete before the capture starts
+        sync.defer = True             # buckets launched from finish() on the capturing thread
         graph = torch.cuda.CUDAGraph()
         # the warm-up's stream: AccumulateGrad nodes stay on it.  thread_local: RCCL's watchdog thread
         # keeps querying its events during the capture (a global-mode capture makes that an error)
