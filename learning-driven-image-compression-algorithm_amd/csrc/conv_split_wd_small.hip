@@ -23,7 +23,13 @@ int wd_dispatch_small(const lic_conv_args& a, hipStream_t s, int& status) {
       return try_split_wd<2, 9, 8, 8, 32, 2, 1, 4>(a, s, status);
     }
   }
-  if (a.mi >= 4 && a.mj >= 4 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8) && blocks(8, 8, 64) >= 32) {
+  // 1x1 convs below the big-map virtual-tap launches (< 64 K px: the 16x16 latents' Swin MLP 128 -> 512
+  // and WBA qkv 192 -> 576, the 32x32 GDN / skip 1x1s) take these tiles too, whatever their channel
+  // count (they went to the register GEMM at ~6 % of peak / 6).  A/B: LIC_WD_SMALL1X1_ALL=0
+  const bool small1x1_all = a.ntaps == 1 && small1x1 && wd_env("LIC_WD_SMALL1X1_ALL", 1) != 0 &&
+                            (int64_t)a.n * a.mi * a.mj < 65536;
+  if (a.mi >= 4 && a.mj >= 4 && (blocks(16, 16, 64) < 256 || a.mi <= 8 || a.mj <= 8 || small1x1_all) &&
+      blocks(8, 8, 64) >= 32) {
     if (a.ntaps == 1 && a.cpad % 32 == 0 && small1x1)
       return try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2, 1>(a, s, status) || try_split_wd<2, 2, 8, 8, 64, 2, 2, 2, 2>(a, s, status);
     if (a.ntaps == 9) {

@@ -45,6 +45,8 @@ SHAPES = [
     ("cc3x3_128_32@16", 128, 32, 3, 1, (1, 1, 1, 1), 16),
     ("cc3x3_224_32@16", 224, 32, 3, 1, (1, 1, 1, 1), 16),
     ("cc1x1_128_32@16", 128, 32, 1, 1, (0, 0, 0, 0), 16),
+    ("qkv1x1@16", 192, 576, 1, 1, (0, 0, 0, 0), 16),
+    ("gdn1x1@32", 192, 192, 1, 1, (0, 0, 0, 0), 32),
 ]
 
 
