@@ -16,13 +16,21 @@ int wd_dispatch_big(const lic_conv_args& a, hipStream_t s, int& status) {
   switch (a.ntaps) {
     case 9:   // 3x3 grids (stride 1, stride-2 phases, ConvT phases): compile-time addressing (GEO 1), else general
       if (bn192 && a.copad == 192 && try_split_wd<2, 9, 16, 16, 192, 4, 2, 3, 0, 1, 0, 2, 2>(a, s, status)) return 1;
+      // 96 channels (the ResidualBottleneck's 3x3 at 64^2): one 4-wave workgroup per tile instead of two
+      // 64-channel blocks, the second half empty (per-element arithmetic unchanged).  A/B: LIC_WD_BN96=0
+      if (a.copad == 96 && wd_env("LIC_WD_BN96", 1) && try_split_wd<2, 9, 16, 16, 96, 4, 1, 6, 0, 1, 0, 2, 2>(a, s, status))
+        return 1;
       if (try_split_wd<2, 9, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status)) return 1;
       return try_split_wd<2, 9, 16, 16, 64, 2, 2, 6>(a, s, status);
-    case 6:   // 3x2 / 2x3 phases (ConvT, stride-2)
+    case 6:   // 3x2 / 2x3 phases (ConvT, stride-2); 192 channels per workgroup as for 3x3 (LIC_WD_BN192)
+      if (bn192 && a.copad == 192 && (try_split_wd<2, 6, 16, 16, 192, 4, 2, 3, 0, 1, 2, 2, 2>(a, s, status) ||
+                                      try_split_wd<2, 6, 16, 16, 192, 4, 2, 3, 0, 1, 3, 2, 2>(a, s, status)))
+        return 1;
       return try_split_wd<2, 6, 16, 16, 64, 2, 2, 6, 0, 1, 2>(a, s, status) ||
              try_split_wd<2, 6, 16, 16, 64, 2, 2, 6, 0, 1, 3>(a, s, status) ||
              try_split_wd<2, 6, 16, 16, 64, 2, 2, 6>(a, s, status);
     case 4:   // 2x2 phases
+      if (bn192 && a.copad == 192 && try_split_wd<2, 4, 16, 16, 192, 4, 2, 3, 0, 1, 0, 2, 2>(a, s, status)) return 1;
       return try_split_wd<2, 4, 16, 16, 64, 2, 2, 6, 0, 1>(a, s, status) || try_split_wd<2, 4, 16, 16, 64, 2, 2, 6>(a, s, status);
     case 2:   // 3x3 s2 phases 1x2 / 2x1
       return try_split_wd<2, 2, 16, 16, 64, 2, 2, 6, 0, 1, 2>(a, s, status) ||

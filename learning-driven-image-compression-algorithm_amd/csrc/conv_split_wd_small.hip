@@ -36,6 +36,12 @@ int wd_dispatch_small(const lic_conv_args& a, hipStream_t s, int& status) {
       // fewer workgroups than the GPU holds (the slice loop's cc / LRP transforms, B x 4 tiles x a few
       // channel blocks): two tap groups of 4 waves per workgroup, half the dependent chain per wave.
       // A/B: LIC_WD_TAPSPLIT=0
+      // 96 output channels per workgroup (3 waves per tap group, three waves per SIMD) where the channel
+      // count allows: the 16x16 latents' 192-channel 3x3s are 256 such workgroups -- one per CU -- instead
+      // of 384 of 64 channels (half the CUs running two).  A/B: LIC_WD_BN96=0
+      if (wd_env("LIC_WD_TAPSPLIT", 1) && wd_env("LIC_WD_BN96", 1) && a.copad % 96 == 0 && blocks(8, 8, 64) <= 512 &&
+          try_split_wd<2, 9, 8, 8, 96, 2, 3, 1, 0, 1, 0, 3, 0, 2>(a, s, status))
+        return 1;
       if (wd_env("LIC_WD_TAPSPLIT", 1) && blocks(8, 8, 64) <= 512 &&
           try_split_wd<2, 9, 8, 8, 64, 2, 2, 1, 0, 1, 0, 0, 0, 2>(a, s, status))
         return 1;

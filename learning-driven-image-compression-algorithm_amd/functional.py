@@ -8,6 +8,7 @@ synchronise.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 import math
 from dataclasses import dataclass, field
@@ -421,6 +422,13 @@ def _accumulate_subpacks(x: Act, subs: Sequence[ConvPack], out: Optional[Act], a
     return out
 
 
+# fp32x6 stride-2 k x k convs run as input-parity phases from this many input pixels (below, the launch
+# takes the exact-fp32 kernel: the hyper analysis' 3x3 s2 convs at 16x16 / 8x8).  Phases from 2048 px
+# gained nothing end to end (1044.7 vs 1042.9 images/s, +9 graph nodes) and moved near-tie symbols of
+# net_unet_ha_hs (profiles/r04/wd_ab.txt), so the threshold stays; A/B: LIC_S2_PHASE_MIN_PIX
+_S2_PHASE_MIN_PIX = int(os.environ.get("LIC_S2_PHASE_MIN_PIX", "16384"))
+
+
 def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT_NONE, slope: float = 0.01,
          epi: int = _ffi.EPI_PLAIN, r1: Optional[Act] = None, g: Optional[Act] = None, r2: Optional[Act] = None,
          y2: Optional[Act] = None, prologue: int = _ffi.PRO_NONE, out_hw=None, shuffle: bool = False,
@@ -428,7 +436,7 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     """Run one ConvPack launch. For convT phases `out` (full map) must be given."""
     if (split_mode() == 2 and x.dtype == torch.float32 and not (force_direct or force_generic or shuffle) and
             epi == _ffi.EPI_PLAIN and r1 is None and g is None and r2 is None and
-            y2 is None and x.B * x.H * x.W >= 16384):
+            y2 is None and x.B * x.H * x.W >= _S2_PHASE_MIN_PIX):
         phases = stride2_phase_packs(pk)
         if phases is not None and len(phases) > 1:
             # fp32x6 stride-2 k x k conv as its four input-parity phases, accumulated in fp32 through
