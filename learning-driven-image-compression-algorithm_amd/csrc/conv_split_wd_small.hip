@@ -49,7 +49,11 @@ int wd_dispatch_small(const lic_conv_args& a, hipStream_t s, int& status) {
       return try_split_wd<2, 9, 8, 8, 64, 2, 2, 2>(a, s, status);
     }
     // one kernel row of a 7x7 (functional.kxk_row_packs): 8 x 14 halo
-    if (a.ntaps == 7) return try_split_wd<2, 7, 8, 8, 64, 2, 2, 2>(a, s, status);
+    if (a.ntaps == 7) {   // (96 channels per workgroup where the count allows, as for 3x3; bit-identical)
+      if (wd_env("LIC_WD_BN96", 1) && a.copad % 96 == 0 && try_split_wd<2, 7, 8, 8, 96, 2, 3, 2, 0, 0, 0, 3>(a, s, status))
+        return 1;
+      return try_split_wd<2, 7, 8, 8, 64, 2, 2, 2>(a, s, status);
+    }
     // stride-2 phases (5x5: 9/6/6/4 taps, 3x3: 4/2/2/1) and ConvT phases onto small maps: compile-time
     // tap grids (3x2 / 2x3 / 2x2 / 1x2 / 2x1) where the taps form one, else the general addressing
     if (a.ntaps == 6)
