@@ -3,7 +3,9 @@ HIP events), aggregated by calling module and op shape.
 
 usage: python tools/layer_profile.py [--arch net_ga] [--batch 32] [--size 256] [--top 40]
 Timings are serialised (no stream overlap), so their sum exceeds the graph-replay
-step time; use them to rank ops, not to predict the step.
+step time; use them to rank ops, not to predict the step.  A wrapped op that calls
+another (GDN.run -> conv) is charged its self time only (the r03 and r04t logs counted
+the nested conv twice).
 """
 import argparse
 import collections
@@ -39,19 +41,29 @@ def _label(name, args):
     return f"{name:14s} {site:40s} {shape}"
 
 
+_NEST = []   # child time of the wrapped ops in flight (Fn.gdn calls Fn.conv: count that time once)
+
+
 def wrap(name):
     fn = getattr(Fn, name)
 
     def w(*args, **kw):
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        _NEST.append(0.0)
         e0.record()
-        out = fn(*args, **kw)
+        try:
+            out = fn(*args, **kw)
+        finally:
+            child = _NEST.pop()
         e1.record()
         e1.synchronize()
+        dt = e0.elapsed_time(e1)
+        if _NEST:
+            _NEST[-1] += dt
         r = REC[_label(name, args)]
         r[0] += 1
-        r[1] += e0.elapsed_time(e1)
+        r[1] += max(0.0, dt - child)   # self time: nested wrapped ops keep their own rows
         if name == "conv" and isinstance(out, Fn.Act) and len(args) > 1:
             pk = args[1]
             mi, mj = kw.get("out_hw") or (out.H, out.W)
