@@ -147,15 +147,17 @@ def dgrad_packs(weight: torch.Tensor, stride: int, pad: Tuple[int, int, int, int
     wd = weight.detach()
     for ry in range(s):
         for rx in range(s):
-            taps = [(ky, kx) for ky in range(kh) for kx in range(kw)
-                    if (ry - (ky - pt)) % s == 0 and (rx - (kx - pl)) % s == 0]
+            # the phase's taps: every s-th kernel row / column from (r + pad) mod s, row-major
+            ky0, kx0 = (ry + pt) % s, (rx + pl) % s
+            kys, kxs = range(ky0, kh, s), range(kx0, kw, s)
+            taps = [(ky, kx) for ky in kys for kx in kxs]
             if not taps:
                 continue
             cpad = Fn._cpad_for(co_pad, dtype)
             copad = Fn._choose_copad(ci)
             w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
-            for t, (ky, kx) in enumerate(taps):
-                w[:ci, t, :co] = wd[:, :, ky, kx].t().to(dtype)
+            # one casting copy of the strided phase view (not two launches per tap: re-packed every step)
+            w[:ci, :, :co].view(ci, len(kys), len(kxs), co).copy_(wd[:, :, ky0::s, kx0::s].permute(1, 2, 3, 0))
             packs.append(ConvPack(w=w, bias=None, ci=co_pad, co=ci,
                                   dy=[(ry - (ky - pt)) // s for ky, kx in taps],
                                   dx=[(rx - (kx - pl)) // s for ky, kx in taps],

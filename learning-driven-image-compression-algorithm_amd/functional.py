@@ -209,18 +209,21 @@ def pack_conv_transpose2d(weight: torch.Tensor, bias: Optional[torch.Tensor], st
     wt = weight.detach()
     for ry in range(s):
         for rx in range(s):
-            kys = [ky for ky in range(kh) if (ry + p - ky) % s == 0]
-            kxs = [kx for kx in range(kw) if (rx + p - kx) % s == 0]
+            # a phase's taps are every s-th row / column of the kernel (ky = (ry + p) mod s, ...)
+            ky0, kx0 = (ry + p) % s, (rx + p) % s
+            kys, kxs = list(range(ky0, kh, s)), list(range(kx0, kw, s))
             # ascending (dy, dx) = descending (ky, kx): a unit-step grid the split kernels address at
             # compile time (conv_split_wd.hip GEO 1)
-            taps = [(ky, kx) for ky in sorted(kys, reverse=True) for kx in sorted(kxs, reverse=True)]
+            taps = [(ky, kx) for ky in reversed(kys) for kx in reversed(kxs)]
             if not taps:
                 continue
             cpad = _cpad_for(ci, dtype)
             copad = _choose_copad(co)
             w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
-            for t, (ky, kx) in enumerate(taps):
-                w[:co, t, :ci] = wt[:, :, ky, kx].t().to(dtype)
+            # the whole phase as one strided view: a flip and one casting copy instead of two
+            # launches per tap (the training path re-packs every step)
+            w[:co, :, :ci].view(co, len(kys), len(kxs), ci).copy_(
+                wt[:, :, ky0::s, kx0::s].flip(2, 3).permute(1, 2, 3, 0))
             dy = [(ry + p - ky) // s - prepad[0] for ky, kx in taps]
             dx = [(rx + p - kx) // s - prepad[1] for ky, kx in taps]
             b = bias.detach().float().contiguous() if bias is not None else None
