@@ -399,6 +399,16 @@ int lic_gdn_bwd_finish(int32_t dtype, const void* x, int32_t ldx, const void* t,
 int lic_lower_bound_sq_bwd(const float* q, const float* dq_eff, int32_t count, float bound, float* dq,
                            int32_t accumulate, lic_stream_t stream);
 
+/* Weight pack into the conv launches' layout dst[copad][nty*ntx][cpad] (dtype, RNE) from an fp32
+ * weight read through signed element strides: dst[o][ty*ntx+tx][c] = src[o*so + c*sc + ty*sy +
+ * tx*sx] for o < no, c < nc, else 0.  One launch per pack: nn.Conv2d [co,ci,kh,kw] (so, sc, sy, sx
+ * = its strides), the dgrad pack (transposed: so <-> sc; mirrored taps: src at the last tap,
+ * sy, sx < 0), stride-s dgrad / ConvTranspose2d phases (sy = s*kw, ...).  The training path
+ * re-packs every weight each step (reference train_net_unet.py:198-199: clip + opt.step, then the next forward). */
+int lic_pack_taps(int32_t dtype, const float* src, int64_t so, int64_t sc, int64_t sy, int64_t sx, int32_t no,
+                  int32_t nc, int32_t nty, int32_t ntx, void* dst, int32_t copad, int32_t cpad,
+                  lic_stream_t stream);
+
 /* Window-attention core backward (WBA layers/win_attention.py:85-116, WMSA
  * model/Block_unet.py:216-252): given the forward args `a` (qkv view, table, mask)
  * and dO (C channels per pixel), writes dqkv (3C channels: dq | dk | dv) and, if

@@ -139,9 +139,10 @@ def dgrad_packs(weight: torch.Tensor, stride: int, pad: Tuple[int, int, int, int
     co, ci, kh, kw = weight.shape
     pt, pl, pb, pr = pad
     if stride == 1:
-        wt = weight.detach().transpose(0, 1).flip(2, 3)
-        return [Fn.pack_conv2d(wt, None, 1, (kh - 1 - pt, kw - 1 - pl, kh - 1 - pb, kw - 1 - pr), dtype,
-                               cin_to=co_pad)]
+        # weights transposed (a view) and taps mirrored (read backwards by the pack launch)
+        return [Fn.pack_conv2d(weight.detach().transpose(0, 1), None, 1,
+                               (kh - 1 - pt, kw - 1 - pl, kh - 1 - pb, kw - 1 - pr), dtype, cin_to=co_pad,
+                               mirror=True)]
     s = stride
     packs = []
     wd = weight.detach()
@@ -155,9 +156,16 @@ def dgrad_packs(weight: torch.Tensor, stride: int, pad: Tuple[int, int, int, int
                 continue
             cpad = Fn._cpad_for(co_pad, dtype)
             copad = Fn._choose_copad(ci)
-            w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
-            # one casting copy of the strided phase view (not two launches per tap: re-packed every step)
-            w[:ci, :, :co].view(ci, len(kys), len(kxs), co).copy_(wd[:, :, ky0::s, kx0::s].permute(1, 2, 3, 0))
+            if wd.is_cuda and wd.dtype == torch.float32:
+                # one launch per phase (re-packed every step)
+                s_co, s_ci, s_y, s_x = wd.stride()
+                w = Fn.pack_taps(wd, ky0 * s_y + kx0 * s_x, s_ci, s_co, s * s_y, s * s_x, ci, co, len(kys),
+                                 len(kxs), copad, cpad, dtype)
+            else:
+                w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
+                # one casting copy of the strided phase view (not two launches per tap)
+                w[:ci, :, :co].view(ci, len(kys), len(kxs), co).copy_(
+                    wd[:, :, ky0::s, kx0::s].permute(1, 2, 3, 0))
             packs.append(ConvPack(w=w, bias=None, ci=co_pad, co=ci,
                                   dy=[(ry - (ky - pt)) // s for ky, kx in taps],
                                   dx=[(rx - (kx - pl)) // s for ky, kx in taps],

@@ -1,0 +1,64 @@
+// Weight packing for the conv kernels' [copad][ntaps][cpad] layout, on the device, in one launch
+// (include/lic.h lic_pack_taps).  The training path re-packs every conv weight at every step --
+// forward pack, transposed + mirrored dgrad pack, stride-s dgrad phases, transposed-conv phases --
+// which torch spelled as a zero fill, a flip and a casting copy per pack (and two launches per tap
+// before that): ~1300 small launches per net_unet_ha_hs step (rocprofv3 trace r04v).  Here every
+// pack is one grid-stride pass that reads the fp32 weight through four signed element strides (a
+// flip is a negative stride, a phase a stride of s taps), writes the zero padding itself and
+// converts with round-to-nearest-even -- the bytes torch's cast produced.
+#include "lic_common.h"
+
+namespace lic {
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_taps_kernel(const float* __restrict__ src, int64_t so, int64_t sc,
+                                                        int64_t sy, int64_t sx, int no, int nc, int nty, int ntx,
+                                                        T* __restrict__ dst, int copad, int cpad) {
+  const int ntap = nty * ntx;
+  const int64_t total = (int64_t)copad * ntap * cpad;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cpad);
+    const int64_t r = i / cpad;
+    const int t = (int)(r % ntap);
+    const int o = (int)(r / ntap);
+    float v = 0.f;
+    if (o < no && c < nc) {
+      const int ty = t / ntx, tx = t - ty * ntx;
+      v = src[o * so + c * sc + ty * sy + tx * sx];
+    }
+    dst[i] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+hipError_t launch_pack(const float* src, int64_t so, int64_t sc, int64_t sy, int64_t sx, int no, int nc, int nty,
+                       int ntx, void* dst, int copad, int cpad, hipStream_t s) {
+  const int64_t total = (int64_t)copad * nty * ntx * cpad;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_taps_kernel<T>, dim3(blocks), dim3(256), 0, s, src, so, sc, sy, sx, no, nc, nty, ntx,
+                     (T*)dst, copad, cpad);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace lic
+
+extern "C" int lic_pack_taps(int32_t dtype, const float* src, int64_t so, int64_t sc, int64_t sy, int64_t sx,
+                             int32_t no, int32_t nc, int32_t nty, int32_t ntx, void* dst, int32_t copad,
+                             int32_t cpad, lic_stream_t stream) {
+  if (!src || !dst) return lic::fail("lic_pack_taps: null pointer");
+  if (no < 0 || nc < 0 || nty <= 0 || ntx <= 0 || copad <= 0 || cpad <= 0 || no > copad || nc > cpad)
+    return lic::fail("lic_pack_taps: bad sizes (need 0 <= no <= copad, 0 <= nc <= cpad, taps > 0)");
+  if ((int64_t)nty * ntx > LIC_MAX_TAPS * 4) return lic::fail("lic_pack_taps: too many taps");
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  switch (dtype) {
+    case LIC_F32: e = lic::launch_pack<float>(src, so, sc, sy, sx, no, nc, nty, ntx, dst, copad, cpad, s); break;
+    case LIC_F16: e = lic::launch_pack<lic::half_t>(src, so, sc, sy, sx, no, nc, nty, ntx, dst, copad, cpad, s); break;
+    case LIC_BF16: e = lic::launch_pack<lic::bf16_t>(src, so, sc, sy, sx, no, nc, nty, ntx, dst, copad, cpad, s); break;
+    default: return lic::fail("lic_pack_taps: dtype must be LIC_F32, LIC_F16 or LIC_BF16");
+  }
+  if (e != hipSuccess) return lic::fail(std::string("lic_pack_taps: ") + hipGetErrorString(e));
+  return 0;
+}

@@ -161,11 +161,26 @@ def _cpad_for(ci: int, dtype: torch.dtype) -> int:
     return -(-ci // bk) * bk
 
 
+def pack_taps(w: torch.Tensor, off: int, so: int, sc: int, sy: int, sx: int, no: int, nc: int, nty: int, ntx: int,
+              copad: int, cpad: int, dtype: torch.dtype) -> torch.Tensor:
+    """lic_pack_taps: dst[copad][nty*ntx][cpad] (dtype) with dst[o][ty*ntx+tx][c] = w[off + o*so + c*sc +
+    ty*sy + tx*sx] (element offsets into w's storage view, signed strides) for o < no, c < nc, zero
+    elsewhere -- one launch per pack (the training path re-packs every weight each step)."""
+    if w.dtype != torch.float32:
+        raise _ffi.LicError("pack_taps: fp32 weights only")
+    dst = torch.empty((copad, nty * ntx, cpad), dtype=dtype, device=w.device)
+    check(_lib().lic_pack_taps(dtype_id(dtype), ctypes.c_void_p(w.data_ptr() + 4 * off), so, sc, sy, sx, no, nc,
+                               nty, ntx, _dp(dst), copad, cpad, stream_handle()))
+    return dst
+
+
 def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad, dtype: torch.dtype,
-                groups: int = 1, cin_to: Optional[int] = None, cpad_to: Optional[int] = None) -> ConvPack:
+                groups: int = 1, cin_to: Optional[int] = None, cpad_to: Optional[int] = None,
+                mirror: bool = False) -> ConvPack:
     """nn.Conv2d weight [co, ci/g, kh, kw] -> packed [copad][kh*kw][cpad]; pad = (top, left, bottom, right).
     cin_to: treat the input as cin_to channels (extra channels known zero; zero weights).
-    cpad_to: an explicit packed channel count (>= cin; e.g. one 8-channel fp32 halo chunk)."""
+    cpad_to: an explicit packed channel count (>= cin; e.g. one 8-channel fp32 halo chunk).
+    mirror: pack weight.flip(2, 3) (the dgrad pack), read in place on the device."""
     co, cig, kh, kw = weight.shape
     pt, pl, pb, pr = pad
     cin = cig if cin_to is None else cin_to
@@ -183,13 +198,17 @@ def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int,
             raise ValueError("pack_conv2d: cpad_to below the channel count or grouped")
         cpad = cpad_to
     copad = _choose_copad(co)
-    # one permute+cast copy kernel (plus a fill when padded): the training path re-packs
-    # every conv each step, so launches count
-    src = weight.detach().permute(0, 2, 3, 1).reshape(co, kh * kw, cig)
-    if copad == co and cpad == cig:
-        w = torch.empty((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
-        w.copy_(src)
+    wd = weight.detach()
+    if wd.is_cuda and wd.dtype == torch.float32:
+        # one launch (padding zeros, mirror and cast included): the training path re-packs every
+        # conv each step, so launches count
+        so, sc, sy, sx = wd.stride()
+        off = 0
+        if mirror:
+            off, sy, sx = (kh - 1) * sy + (kw - 1) * sx, -sy, -sx
+        w = pack_taps(wd, off, so, sc, sy, sx, co, cig, kh, kw, copad, cpad, dtype)
     else:
+        src = (wd.flip(2, 3) if mirror else wd).permute(0, 2, 3, 1).reshape(co, kh * kw, cig)
         w = torch.zeros((copad, kh * kw, cpad), dtype=dtype, device=weight.device)
         w[:co, :, :cig].copy_(src)
     dy = [ky - pt for ky in range(kh) for kx in range(kw)]
@@ -219,11 +238,16 @@ def pack_conv_transpose2d(weight: torch.Tensor, bias: Optional[torch.Tensor], st
                 continue
             cpad = _cpad_for(ci, dtype)
             copad = _choose_copad(co)
-            w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
-            # the whole phase as one strided view: a flip and one casting copy instead of two
-            # launches per tap (the training path re-packs every step)
-            w[:co, :, :ci].view(co, len(kys), len(kxs), ci).copy_(
-                wt[:, :, ky0::s, kx0::s].flip(2, 3).permute(1, 2, 3, 0))
+            if wt.is_cuda and wt.dtype == torch.float32:
+                # one launch per phase: taps every s-th row / column, read backwards from the last
+                s_ci, s_co, s_y, s_x = wt.stride()
+                w = pack_taps(wt, kys[-1] * s_y + kxs[-1] * s_x, s_co, s_ci, -s * s_y, -s * s_x, co, ci,
+                              len(kys), len(kxs), copad, cpad, dtype)
+            else:
+                w = torch.zeros((copad, len(taps), cpad), dtype=dtype, device=weight.device)
+                # the whole phase as one strided view (not two launches per tap)
+                w[:co, :, :ci].view(co, len(kys), len(kxs), ci).copy_(
+                    wt[:, :, ky0::s, kx0::s].flip(2, 3).permute(1, 2, 3, 0))
             dy = [(ry + p - ky) // s - prepad[0] for ky, kx in taps]
             dx = [(rx + p - kx) // s - prepad[1] for ky, kx in taps]
             b = bias.detach().float().contiguous() if bias is not None else None
