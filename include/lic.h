@@ -409,6 +409,16 @@ int lic_pack_taps(int32_t dtype, const float* src, int64_t so, int64_t sc, int64
                   int32_t nc, int32_t nty, int32_t ntx, void* dst, int32_t copad, int32_t cpad,
                   lic_stream_t stream);
 
+/* Many lic_pack_taps in one launch (a training step's packs, replayed in a hipGraph): `desc` is
+ * DEVICE memory holding n descriptors of LIC_PACK_DESC_WORDS int64 each,
+ *   { src, dst, so, sc, sy, sx, no, nc, nty, ntx, copad, cpad, dtype, first_block, 0, 0 },
+ * ascending first_block; descriptor i owns blocks [first_block_i, first_block_{i+1}) of
+ * lic_pack_block_elems() elements each (ceil(copad*nty*ntx*cpad / that)); nblocks = the total.
+ * The caller validates the descriptors (the library cannot read device memory on the host).      */
+#define LIC_PACK_DESC_WORDS 16
+int32_t lic_pack_block_elems(void);
+int lic_pack_taps_batch(const int64_t* desc, int32_t n, int32_t nblocks, lic_stream_t stream);
+
 /* Window-attention core backward (WBA layers/win_attention.py:85-116, WMSA
  * model/Block_unet.py:216-252): given the forward args `a` (qkv view, table, mask)
  * and dO (C channels per pixel), writes dqkv (3C channels: dq | dk | dv) and, if

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "lic_rate_train_parts", "lic_rate_train_fwd", "lic_rate_train_bwd", "lic_recon_train_blocks",
     "lic_recon_train_fwd", "lic_recon_train_bwd", "lic_dwconv_wgrad_workspace", "lic_dwconv_wgrad",
     "lic_resunit_fwd", "lic_patches", "lic_wba_qkv_attn_fwd", "lic_pack_taps",
+    "lic_pack_taps_batch", "lic_pack_block_elems",
 )
 LIC_EB_PARAMS = 58
 
@@ -201,6 +202,8 @@ def load():
         "lic_conv2d_fwd": [V, V],
         "lic_gdn_prepare": [I, V, V, I, F, F, F, V, I, I, V, V],
         "lic_pack_taps": [I, V, L, L, L, L, I, I, I, I, V, I, I, V],
+        "lic_pack_taps_batch": [V, I, I, V],
+        "lic_pack_block_elems": [],
         "lic_win_attn_fwd": [V, V],
         "lic_layernorm_fwd": [I, V, I, I, I, V, V, F, V, I, V],
         "lic_gauss_rate_fwd": [V, V],

@@ -686,8 +686,8 @@ class _DwConvFn(torch.autograd.Function):
             if stride != 1:
                 raise NotImplementedError("depthwise conv backward: stride 1 only (Syntax_Model)")
             pt, pl, pb, pr = pad
-            pk = Fn.pack_conv2d(weight.detach().flip(2, 3), None, 1,
-                                (kh - 1 - pt, kw - 1 - pl, kh - 1 - pb, kw - 1 - pr), g.dtype, groups=C)
+            pk = Fn.pack_conv2d(weight.detach(), None, 1, (kh - 1 - pt, kw - 1 - pl, kh - 1 - pb, kw - 1 - pr),
+                                g.dtype, groups=C, mirror=True)
             dx = Fn.conv(Act(g), pk, out_hw=(H, W)).t
         if ctx.needs_input_grad[1]:
             tdy, tdx = _taps(kh, kw, pad[0], pad[1])

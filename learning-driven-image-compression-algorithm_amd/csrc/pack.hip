@@ -41,8 +41,64 @@ hipError_t launch_pack(const float* src, int64_t so, int64_t sc, int64_t sy, int
   return hipGetLastError();
 }
 
+// All of a step's packs in one launch: desc = n descriptors of LIC_PACK_DESC_WORDS int64 each
+// (include/lic.h), sorted by first_block; block b packs elements [(b - first_block) * PACK_BLOCK_ELEMS, +
+// PACK_BLOCK_ELEMS) of the descriptor whose block range holds b (binary search).
+constexpr int PACK_BLOCK_ELEMS = 2048;
+
+template <typename T>
+__device__ __forceinline__ void pack_span(const float* __restrict__ src, int64_t so, int64_t sc, int64_t sy, int64_t sx,
+                                          int no, int nc, int ntx, int ntap, int cpad, T* __restrict__ dst,
+                                          int64_t base, int64_t total) {
+  for (int k = threadIdx.x; k < PACK_BLOCK_ELEMS; k += blockDim.x) {
+    const int64_t i = base + k;
+    if (i >= total) break;
+    const int c = (int)(i % cpad);
+    const int64_t r = i / cpad;
+    const int t = (int)(r % ntap);
+    const int o = (int)(r / ntap);
+    float v = 0.f;
+    if (o < no && c < nc) {
+      const int ty = t / ntx, tx = t - ty * ntx;
+      v = src[o * so + c * sc + ty * sy + tx * sx];
+    }
+    dst[i] = from_f<T>(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_taps_batch_kernel(const int64_t* __restrict__ desc, int n) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[(int64_t)mid * LIC_PACK_DESC_WORDS + 13] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t* d = desc + (int64_t)lo * LIC_PACK_DESC_WORDS;
+  const float* src = (const float*)d[0];
+  void* dst = (void*)d[1];
+  const int no = (int)d[6], nc = (int)d[7], nty = (int)d[8], ntx = (int)d[9], copad = (int)d[10], cpad = (int)d[11];
+  const int dtype = (int)d[12];
+  const int ntap = nty * ntx;
+  const int64_t total = (int64_t)copad * ntap * cpad;
+  const int64_t base = (int64_t)(b - (int)d[13]) * PACK_BLOCK_ELEMS;
+  if (dtype == LIC_F16) pack_span<half_t>(src, d[2], d[3], d[4], d[5], no, nc, ntx, ntap, cpad, (half_t*)dst, base, total);
+  else if (dtype == LIC_BF16) pack_span<bf16_t>(src, d[2], d[3], d[4], d[5], no, nc, ntx, ntap, cpad, (bf16_t*)dst, base, total);
+  else pack_span<float>(src, d[2], d[3], d[4], d[5], no, nc, ntx, ntap, cpad, (float*)dst, base, total);
+}
+
 }  // namespace
 }  // namespace lic
+
+extern "C" int32_t lic_pack_block_elems(void) { return lic::PACK_BLOCK_ELEMS; }
+
+extern "C" int lic_pack_taps_batch(const int64_t* desc, int32_t n, int32_t nblocks, lic_stream_t stream) {
+  if (!desc || n <= 0 || nblocks <= 0) return lic::fail("lic_pack_taps_batch: need descriptors and blocks");
+  hipLaunchKernelGGL(lic::pack_taps_batch_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, desc, n);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return lic::fail(std::string("lic_pack_taps_batch: ") + hipGetErrorString(e));
+  return 0;
+}
 
 extern "C" int lic_pack_taps(int32_t dtype, const float* src, int64_t so, int64_t sc, int64_t sy, int64_t sx,
                              int32_t no, int32_t nc, int32_t nty, int32_t ntx, void* dst, int32_t copad,

@@ -168,10 +168,84 @@ def pack_taps(w: torch.Tensor, off: int, so: int, sc: int, sy: int, sx: int, no:
     elsewhere -- one launch per pack (the training path re-packs every weight each step)."""
     if w.dtype != torch.float32:
         raise _ffi.LicError("pack_taps: fp32 weights only")
+    plan = _PACK_PLAN
+    key = (w.data_ptr() + 4 * off, so, sc, sy, sx, no, nc, nty, ntx, copad, cpad, dtype_id(dtype))
+    if plan is not None and plan.mode == "replay":
+        return plan.take(key)
     dst = torch.empty((copad, nty * ntx, cpad), dtype=dtype, device=w.device)
-    check(_lib().lic_pack_taps(dtype_id(dtype), ctypes.c_void_p(w.data_ptr() + 4 * off), so, sc, sy, sx, no, nc,
+    check(_lib().lic_pack_taps(dtype_id(dtype), ctypes.c_void_p(key[0]), so, sc, sy, sx, no, nc,
                                nty, ntx, _dp(dst), copad, cpad, stream_handle()))
+    if plan is not None and plan.mode == "record":
+        plan.items.append((key, dst))
     return dst
+
+
+class PackPlan:
+    """A training step's weight packs as ONE launch (lic_pack_taps_batch).  Weights change only at
+    the optimiser step, so every pack of a step can be written at its start.  ``record()`` around
+    an eager step notes each pack_taps call (source, strides, sizes) and keeps its output buffer;
+    ``finalize()`` uploads the descriptor table; then, per captured / replayed step,
+    ``launch_all()`` refreshes every buffer in one launch and ``replay()`` makes pack_taps hand the
+    buffers back in call order -- checking each call against the recorded one and raising on any
+    difference (a different call sequence cannot silently read another layer's weights)."""
+
+    def __init__(self):
+        self.mode = None
+        self.items = []
+        self.i = 0
+        self.desc = None
+        self.nblocks = 0
+
+    def __enter__(self):
+        global _PACK_PLAN
+        if _PACK_PLAN is not None:
+            raise _ffi.LicError("PackPlan: another plan is active")
+        _PACK_PLAN = self
+        return self
+
+    def __exit__(self, *exc):
+        global _PACK_PLAN
+        _PACK_PLAN = None
+        mode, self.mode = self.mode, None
+        if mode == "replay" and exc[0] is None and self.i != len(self.items):
+            raise _ffi.LicError(f"PackPlan: step used {self.i} of {len(self.items)} recorded packs")
+        return False
+
+    def record(self) -> "PackPlan":
+        self.mode, self.items = "record", []
+        return self
+
+    def replay(self) -> "PackPlan":
+        if self.desc is None:
+            raise _ffi.LicError("PackPlan: finalize() before replay()")
+        self.mode, self.i = "replay", 0
+        return self
+
+    def take(self, key) -> torch.Tensor:
+        if self.i >= len(self.items) or self.items[self.i][0] != key:
+            raise _ffi.LicError(f"PackPlan: pack call {self.i} differs from the recorded step")
+        self.i += 1
+        return self.items[self.i - 1][1]
+
+    def finalize(self) -> None:
+        if not self.items:
+            raise _ffi.LicError("PackPlan: nothing recorded")
+        per = int(_lib().lic_pack_block_elems())
+        rows, first = [], 0
+        for key, dst in self.items:
+            src, so, sc, sy, sx, no, nc, nty, ntx, copad, cpad, dt = key
+            rows.append([src, dst.data_ptr(), so, sc, sy, sx, no, nc, nty, ntx, copad, cpad, dt, first, 0, 0])
+            first += -(-(copad * nty * ntx * cpad) // per)
+        if first >= 2 ** 31:
+            raise _ffi.LicError("PackPlan: too many blocks")
+        self.desc = torch.tensor(rows, dtype=torch.int64).to(self.items[0][1].device)
+        self.nblocks = first
+
+    def launch_all(self) -> None:
+        check(_lib().lic_pack_taps_batch(_dp(self.desc), len(self.items), self.nblocks, stream_handle()))
+
+
+_PACK_PLAN: Optional[PackPlan] = None
 
 
 def pack_conv2d(weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad, dtype: torch.dtype,

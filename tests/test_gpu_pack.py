@@ -45,6 +45,9 @@ def test_pack_conv2d_groups_and_cpad_to(dtype):
     w = _weight((64, 1, 3, 3), 3)
     _same([Fn.pack_conv2d(w.to(DEV), None, 1, (1, 1, 1, 1), dtype, groups=64)],
           [Fn.pack_conv2d(w, None, 1, (1, 1, 1, 1), dtype, groups=64)])
+    # the depthwise dgrad pack (mirrored taps, read in place)
+    _same([Fn.pack_conv2d(w.to(DEV), None, 1, (1, 1, 1, 1), dtype, groups=64, mirror=True)],
+          [Fn.pack_conv2d(w, None, 1, (1, 1, 1, 1), dtype, groups=64, mirror=True)])
     w = _weight((32, 3, 3, 3), 4)
     _same([Fn.pack_conv2d(w.to(DEV), None, 2, (0, 0, 1, 1), dtype, cpad_to=8)],
           [Fn.pack_conv2d(w, None, 2, (0, 0, 1, 1), dtype, cpad_to=8)])
@@ -74,3 +77,37 @@ def test_pack_taps_rejects_bad_sizes():
     w = torch.zeros(8, 8, 3, 3, device=DEV)
     with pytest.raises(Exception):
         Fn.pack_taps(w, 0, 72, 9, 3, 1, 16, 8, 3, 3, 8, 8, torch.float16)   # no > copad
+
+
+def test_pack_plan_batch_equals_direct_packs():
+    """PackPlan: record a step's packs, change the weights in place (the optimiser step), then one
+    lic_pack_taps_batch launch + replay hand back buffers equal to fresh direct packs; a call
+    sequence that differs from the recorded one raises."""
+    ws = [_weight((192, 192, 3, 3), 11).to(DEV), _weight((128, 64, 5, 5), 12).to(DEV),
+          _weight((192, 192, 5, 5), 13).to(DEV), _weight((320, 128, 1, 1), 14).to(DEV)]
+
+    def packs():
+        out = [Fn.pack_conv2d(ws[0], None, 1, (1, 1, 1, 1), torch.bfloat16)]
+        out += AG.dgrad_packs(ws[0], 1, (1, 1, 1, 1), torch.bfloat16, 192)
+        out += AG.dgrad_packs(ws[1], 2, (1, 1, 2, 2), torch.float16, 128)
+        out += Fn.pack_conv_transpose2d(ws[2], None, 2, 3, 1, torch.bfloat16, (1, 1))
+        out += [Fn.pack_conv2d(ws[3], None, 1, (0, 0, 0, 0), torch.float32)]
+        return out
+
+    plan = Fn.PackPlan()
+    with plan.record():
+        rec = packs()
+    plan.finalize()
+    for w in ws:
+        w.mul_(-1.5).add_(0.01)
+    plan.launch_all()
+    with plan.replay():
+        got = packs()
+    ref = packs()
+    torch.cuda.synchronize()
+    assert len(got) == len(ref) == len(rec)
+    for g, r in zip(got, ref):
+        assert torch.equal(g.w, r.w)
+    with pytest.raises(Exception):
+        with plan.replay():
+            Fn.pack_conv2d(ws[1], None, 1, (2, 2, 2, 2), torch.bfloat16)    # not the recorded first call

@@ -24,6 +24,7 @@ Differences:
 JSON line (images/s of the whole job, MAX step time over ranks).
 """
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -93,6 +94,7 @@ def main():
         # one process per GPU, started before this process touches the GPU (no re-exec)
         sys.exit(D.launch_workers([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
     from lic_amd.model import net_ga, net_unet_ha_hs
+    from lic_amd import functional as Fn
     rank, world, local = D.init("nccl")
     if D.launched() and args.gpus > 1 and world != args.gpus:
         raise SystemExit(f"train_net_unet.py: --gpus {args.gpus} but the launcher started {world} ranks")
@@ -143,11 +145,16 @@ def main():
         seed_t = torch.zeros((1,), dtype=torch.int64, device=dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream())
+        # every weight pack of the step in one launch at its start (functional.PackPlan): the last
+        # warm-up step (caches already warm) records them, the captured step replays them
+        plan = Fn.PackPlan() if os.environ.get("LIC_PACK_PLAN", "1") != "0" else None
+        nwarm = max(2 if plan is not None else 1, args.warmup)
         with torch.cuda.stream(side):
-            for _ in range(max(1, args.warmup)):
+            for k in range(nwarm):
                 opt.zero_grad(set_to_none=True)
-                bpp, mse = net(static_x, "train", seed_dev=seed_t)
-                (args.lmbda * 255 ** 2 * mse + bpp).backward()
+                with plan.record() if (plan is not None and k == nwarm - 1) else contextlib.nullcontext():
+                    bpp, mse = net(static_x, "train", seed_dev=seed_t)
+                    (args.lmbda * 255 ** 2 * mse + bpp).backward()
                 sync.finish()              # first collectives eagerly: communicator set up before capture
                 grad_params = [p for p in params if p.grad is not None]
                 torch.nn.utils.clip_grad_norm_(grad_params, 1.0)
@@ -155,13 +162,18 @@ def main():
                 seed_t.add_(1)
         torch.cuda.current_stream().wait_stream(side)
         opt.zero_grad(set_to_none=True)
+        if plan is not None:
+            plan.finalize()
         torch.cuda.synchronize(dev)   # the warm-up's collectives complete before the capture starts
         sync.defer = True             # buckets launched from finish() on the capturing thread
         graph = torch.cuda.CUDAGraph()
         # the warm-up's stream: AccumulateGrad nodes stay on it.  thread_local: RCCL's watchdog thread
         # keeps querying its events during the capture (a global-mode capture makes that an error)
         with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
-            outs = step_body(static_x, seed_t)
+            if plan is not None:
+                plan.launch_all()
+            with plan.replay() if plan is not None else contextlib.nullcontext():
+                outs = step_body(static_x, seed_t)
             seed_t.add_(1)
 
         def step():
