@@ -77,10 +77,16 @@ def synthetic_kodak():
             for i in range(24)]
 
 
-def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=False, graph=True, reps=1,
-             device="cuda"):
+def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp32x6", is_high=False, graph=True, reps=1,
+             device="cuda", batched=True):
     """BASELINE config 4: every lambda x every synthetic Kodak image, images sharded
-    round-robin over ranks.  Returns (per-lambda summaries, images/s) on rank 0."""
+    round-robin over ranks.  Returns (per-lambda summaries, images/s) on rank 0.
+
+    batched (default): per lambda, each rank's images of one shape (Kodak: 18 landscape 768x512, 6
+    portrait 512x768) run as ONE batch -- one net and one captured hipGraph per (lambda, shape); the
+    summaries are the same per-image means (bpp of a batch of equal-sized images is the mean of their
+    bpps; PSNR is the mean of per-image PSNRs, net_ga.py:1141-1142).  batched=False: one image per
+    forward (the reference's loop).  Default precision: fp32x6, the bench's gated fp32-grade path."""
     from lic_amd.model import net_ga, net_unet_ha_hs
     from lic_amd import distributed as D
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
@@ -89,53 +95,59 @@ def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=Fals
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     mine = D.shard(synthetic_kodak(), rank, world)
+    # shape -> padded [B, 3, H, W] batch in [-1, 1], in first-seen order
+    groups = []
+    for name, img in mine:
+        data, h, w = pad64(img)
+        x = data.unsqueeze(0) * 2.0 - 1.0
+        for grp in groups:
+            if grp[0] == (h, w):
+                grp[1].append(x)
+                break
+        else:
+            groups.append(((h, w), [x]))
+    batches = [(hw, torch.cat(xs, 0).to(device)) for hw, xs in groups]
     summaries, total_time = [], 0.0
-    keep = []  # every (net, graph) stays alive until the sweep ends (no graph teardown mid-sweep)
     for li, lmbda in enumerate(lambdas):
-        nets, graphs = {}, {}
-        keep.append((nets, graphs))
-        sums = [0.0, 0.0, 0.0, 0.0]  # bpp, psnr, mse, rd
-        for name, img in mine:
-            _, h, w = img.shape
-            data, h, w = pad64(img)
-            x = (data.unsqueeze(0) * 2.0 - 1.0).to(device)
-            key = tuple(x.shape)
-            if key not in nets:
-                torch.manual_seed(li)
-                net = mod.Net((1, h, w, 3), (1, h, w, 3), is_high, False, precision=precision).to(device)
-                wp = weight_path.format(lmbda=lmbda) if weight_path else ""
-                if wp and os.path.exists(wp):
-                    net.load_state_dict(torch.load(wp, map_location="cpu", weights_only=True), strict=True)
-                else:
-                    net_ga.synthetic_syntax_bias_(net, li)
-                xin = torch.empty_like(x)
-                nets[key] = (net, xin)
-                if graph:
-                    xin.copy_(x)
+        sums = [0.0, 0.0, 0.0, 0.0]  # bpp, psnr, mse, rd (sums over images)
+        for (h, w), X in batches:
+            B = X.shape[0] if batched else 1
+            torch.manual_seed(li)
+            net = mod.Net((B, h, w, 3), (B, h, w, 3), is_high, False, precision=precision).to(device)
+            wp = weight_path.format(lmbda=lmbda) if weight_path else ""
+            if wp and os.path.exists(wp):
+                net.load_state_dict(torch.load(wp, map_location="cpu", weights_only=True), strict=True)
+            else:
+                net_ga.synthetic_syntax_bias_(net, li)
+            xin = X[:B].clone()
+            g = out = None
+            if graph:
+                net(xin, 'test')
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
                     net(xin, 'test')
-                    s = torch.cuda.Stream()
-                    s.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.stream(s):
-                        net(xin, 'test')
-                    torch.cuda.current_stream().wait_stream(s)
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g):
-                        out = net(xin, 'test')
-                    graphs[key] = (g, out)
-            net, xin = nets[key]
-            xin.copy_(x)
+                torch.cuda.current_stream().wait_stream(s)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    out = net(xin, 'test')
+            for i0 in range(0, X.shape[0], B):
+                xin.copy_(X[i0:i0 + B])
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    if graph:
+                        g.replay()
+                        bpp, v_mse, v_psnr = out
+                    else:
+                        bpp, v_mse, v_psnr = net(xin, 'test')
+                torch.cuda.synchronize()
+                total_time += (time.perf_counter() - t0) / reps
+                b, p, msum = bpp.item(), v_psnr.item(), v_mse.double().sum().item()
+                sums[0] += B * b; sums[1] += B * p; sums[2] += msum; sums[3] += B * b + lmbda * msum
+            # the graph before the net whose buffers it replays; memory back before the next shape
+            del g, out, net, xin
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                if graph:
-                    graphs[key][0].replay()
-                    bpp, v_mse, v_psnr = graphs[key][1]
-                else:
-                    bpp, v_mse, v_psnr = net(xin, 'test')
-            torch.cuda.synchronize()
-            total_time += (time.perf_counter() - t0) / reps
-            b, m, p = bpp.item(), v_mse.mean().item(), v_psnr.item()
-            sums[0] += b; sums[1] += p; sums[2] += m; sums[3] += b + lmbda * m
         sums = D.sum_over_ranks(sums + [len(mine)], world, device)
         cnt = sums[4]
         summaries.append({"lambda": lmbda, "bpp": sums[0] / cnt, "psnr": sums[1] / cnt, "mse": sums[2] / cnt,
@@ -147,9 +159,6 @@ def rd_sweep(lambdas, weight_path, arch="net_ga", precision="fp16", is_high=Fals
     elapsed = D.max_over_ranks(total_time, world, device)
     n_img = len(lambdas) * 24
     torch.cuda.synchronize()
-    for nets, graphs in keep:   # graphs before the nets whose buffers they replay
-        graphs.clear()
-    keep.clear()
     D.finish(world)
     return summaries, n_img / elapsed, world
 
@@ -250,9 +259,14 @@ def main(argv=None):
     parser.add_argument("--lambdas", default=",".join(str(v) for v in RD_LAMBDAS),
                         help="comma-separated lambda list for --synthetic-kodak")
     parser.add_argument("--graph", action="store_true", help="hipGraph replay per (lambda, shape)")
+    parser.add_argument("--per-image", action="store_true", dest="per_image",
+                        help="--synthetic-kodak: one image per forward instead of one batch per image shape")
     parser.add_argument("--gpus", type=int, default=1,
                         help="ranks (one per GPU); without torchrun this process starts them itself")
     args = parser.parse_args(argv)
+    # the sweep defaults to the bench's fp32-grade fp32x6; the single-image CLI keeps exact fp32
+    args.precision_given = any(a == "--precision" or a.startswith("--precision=")
+                               for a in (sys.argv[1:] if argv is None else argv))
     from lic_amd import distributed as D
     if args.gpus > 1 and not D.launched():
         # one process per GPU, started before this process touches the GPU (no re-exec)
@@ -262,12 +276,14 @@ def main(argv=None):
         raise SystemExit(f"eval_net.py: --gpus {args.gpus} but the launcher started {D.env_rank()[1]} ranks")
     if args.synthetic_kodak:
         lambdas = [float(v) for v in args.lambdas.split(",") if v]
-        summ, ips, world = rd_sweep(lambdas, args.weight_path, arch=args.arch, precision=args.precision,
-                                    is_high=args.high, graph=args.graph)
+        prec = args.precision if args.precision_given else "fp32x6"
+        summ, ips, world = rd_sweep(lambdas, args.weight_path, arch=args.arch, precision=prec,
+                                    is_high=args.high, graph=args.graph, batched=not args.per_image)
         if int(os.environ.get("RANK", 0)) == 0:
             print(json.dumps({"metric": "images/sec encode+decode (Kodak-24 R-D sweep, 768x512)",
                               "value": round(ips, 2), "unit": "images/s", "n_gpus": world,
-                              "arch": args.arch, "precision": args.precision, "graph": args.graph,
+                              "arch": args.arch, "precision": prec, "graph": args.graph,
+                              "batching": "per image" if args.per_image else "one batch per (lambda, image shape)",
                               "data": "synthetic Kodak-shaped images, seeded weights per lambda",
                               "rd": summ}), flush=True)
         return

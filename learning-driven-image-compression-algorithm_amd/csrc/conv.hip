@@ -27,12 +27,23 @@ int try_halo(const lic_conv_args& a, hipStream_t s, int& status);
 int conv_halo_split_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
 int conv_split_wd_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
 int conv_split_1x1_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
+// 16-bit stride-1 3x3 / 7x7 on big maps (conv16.h, instantiated in conv16_{f16,bf16}.hip)
+template <typename T> int conv16_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
+// 16-bit 1x1 convolutions on big maps (gemm16.h, gemm16_{f16,bf16}.hip)
+template <typename T> int gemm16_dispatch(const lic_conv_args& a, hipStream_t s, int& status);
 
 // Halo tile choice: the largest output-channel block whose grid still fills the
 // chip (>= 200 workgroups of 16x16 pixels), then 8x8-pixel tiles for small maps
 // (the 16x16 latents of the slice loop).
 template <typename T>
 static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
+  if constexpr (sizeof(T) == 2) {   // round-5 16-bit kernels first
+    if (a.ntaps == 1) {
+      if (int r = gemm16_dispatch<T>(a, s, status)) return r;
+    } else if (int r = conv16_dispatch<T>(a, s, status)) {
+      return r;
+    }
+  }
   const bool gemm_ok = a.ntaps == 1 && (HALO_1X1 == 2 || (HALO_1X1 == 1 && sizeof(T) == 4));
   if (a.groups != 1 || (a.ntaps < 2 && !gemm_ok) || a.prologue != LIC_PRO_NONE || a.force_direct) return 0;
   auto blocks = [&](int th, int tw, int bn) {

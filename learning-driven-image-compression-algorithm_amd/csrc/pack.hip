@@ -48,6 +48,17 @@ hipError_t launch_pack(const float* src, int64_t so, int64_t sc, int64_t sy, int
   return hipGetLastError();
 }
 
+// The kernels index the source with 32-bit element offsets: every stride and the farthest element
+// the view can reach must fit.
+bool pack_strides_fit(int64_t so, int64_t sc, int64_t sy, int64_t sx, int no, int nc, int nty, int ntx) {
+  const int64_t lim = ((int64_t)1 << 31) - 1;
+  auto mag = [](int64_t v) { return v < 0 ? -v : v; };
+  if (mag(so) > lim || mag(sc) > lim || mag(sy) > lim || mag(sx) > lim) return false;
+  const int64_t reach = mag((int64_t)(no > 0 ? no - 1 : 0) * so) + mag((int64_t)(nc > 0 ? nc - 1 : 0) * sc) +
+                        mag((int64_t)(nty - 1) * sy) + mag((int64_t)(ntx - 1) * sx);
+  return reach <= lim;
+}
+
 // All of a step's packs in one launch: desc = n descriptors of LIC_PACK_DESC_WORDS int64 each
 // (include/lic.h), sorted by first_block; block b packs elements [(b - first_block) * PACK_BLOCK_ELEMS, +
 // PACK_BLOCK_ELEMS) of the descriptor whose block range holds b (binary search).
@@ -104,6 +115,8 @@ extern "C" int lic_pack_taps(int32_t dtype, const float* src, int64_t so, int64_
     return lic::fail("lic_pack_taps: bad sizes (need 0 <= no <= copad, 0 <= nc <= cpad, taps > 0)");
   if ((int64_t)nty * ntx > LIC_MAX_TAPS * 4) return lic::fail("lic_pack_taps: too many taps");
   if ((int64_t)copad * nty * ntx * cpad >= ((int64_t)1 << 31)) return lic::fail("lic_pack_taps: pack of 2^31 elements or more");
+  if (!lic::pack_strides_fit(so, sc, sy, sx, no, nc, nty, ntx))
+    return lic::fail("lic_pack_taps: source strides or extent do not fit 32-bit element offsets");
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   switch (dtype) {

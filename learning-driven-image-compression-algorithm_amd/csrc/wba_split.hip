@@ -405,7 +405,13 @@ extern "C" int lic_wba_qkv_attn_fwd(const lic_wba_args* a, lic_stream_t stream) 
   if (!a->x || !a->out || !a->qkv_wsplit || !a->qkv_bias || !a->table || (a->proj_wsplit && !a->proj_bias))
     return fail("wba: null pointer");
   if (a->proj_wsplit && ((uintptr_t)a->proj_wsplit & 15)) return fail("wba: proj pack not 16-byte aligned");
-  if (a->proj_wsplit && (const void*)a->out == (const void*)a->x) return fail("wba: out must not alias x (the shortcut)");
+  {   // the persistent walker prefetches the next window of x while other workgroups store: out may not
+      // overlap x in either mode (and x is the proj shortcut with proj_wsplit)
+    const int64_t npix = (int64_t)a->n * a->h * a->w;
+    const uintptr_t x0 = (uintptr_t)a->x, x1 = x0 + (uintptr_t)(((npix - 1) * a->ldx + WB_C) * 4);
+    const uintptr_t o0 = (uintptr_t)a->out, o1 = o0 + (uintptr_t)(((npix - 1) * a->ldo + WB_C) * 4);
+    if (x0 < o1 && o0 < x1) return fail("wba: out must not overlap x");
+  }
   if (a->ldx < WB_C || a->ldx % 4 || a->ldo < WB_C || a->ldo % 4 || ((uintptr_t)a->x & 15) || ((uintptr_t)a->out & 15) ||
       ((uintptr_t)a->qkv_wsplit & 15))
     return fail("wba: x / out need 16-byte aligned rows (ld a multiple of 4, >= 192)");

@@ -12,6 +12,7 @@ started without torchrun spawn their N ranks themselves (``launch_workers``).
 from __future__ import annotations
 
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -44,13 +45,28 @@ def launch_workers(cmd: Sequence[str], n: int, poll_s: float = 0.2) -> int:
     terminated; returns the first non-zero exit status (0 when every rank succeeded)."""
     if n < 1:
         raise ValueError(f"need at least one worker, got {n}")
-    port = _free_port()
+    # the launcher hosts the rendezvous store itself, the way torchrun's agent does: it binds an
+    # ephemeral port and keeps it for the children's lifetime (no probe-then-release race), and the
+    # ranks' env:// rendezvous connects to it as clients (TORCHELASTIC_USE_AGENT_STORE)
+    store = dist.TCPStore("127.0.0.1", 0, n, True, wait_for_workers=False)
+    port = store.port
     procs = []
+
+    def _stop(signum, frame):   # SIGTERM / SIGINT to the launcher: take the ranks down with it
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        raise SystemExit(128 + signum)
+
+    old = {sig: signal.signal(sig, _stop) for sig in (signal.SIGTERM, signal.SIGINT)}
     try:
         for r in range(n):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-            procs.append(subprocess.Popen(list(cmd), env=env, stdout=None if r == 0 else sys.stderr))
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       TORCHELASTIC_USE_AGENT_STORE="True")
+            # ranks > 0 write their stdout to the launcher's stderr descriptor (fd 2 works whatever
+            # object sys.stderr is, e.g. under pytest capture)
+            procs.append(subprocess.Popen(list(cmd), env=env, stdout=None if r == 0 else 2))
         status = 0
         live = set(range(n))
         while live:
@@ -69,6 +85,8 @@ def launch_workers(cmd: Sequence[str], n: int, poll_s: float = 0.2) -> int:
                 time.sleep(poll_s)
         return status
     finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
         for p in procs:
             if p.poll() is None:
                 p.kill()

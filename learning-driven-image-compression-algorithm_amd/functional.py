@@ -234,6 +234,11 @@ class PackPlan:
         rows, first = [], 0
         for key, dst in self.items:
             src, so, sc, sy, sx, no, nc, nty, ntx, copad, cpad, dt = key
+            # the batch kernel reads its descriptors with 32-bit offsets and cannot check them itself
+            reach = (abs(max(no - 1, 0) * so) + abs(max(nc - 1, 0) * sc) + abs((nty - 1) * sy) +
+                     abs((ntx - 1) * sx))
+            if max(abs(so), abs(sc), abs(sy), abs(sx), reach) >= 2 ** 31:
+                raise _ffi.LicError("PackPlan: source strides / extent do not fit 32-bit offsets")
             rows.append([src, dst.data_ptr(), so, sc, sy, sx, no, nc, nty, ntx, copad, cpad, dt, first, 0, 0])
             first += -(-(copad * nty * ntx * cpad) // per)
         if first >= 2 ** 31:

@@ -85,7 +85,10 @@ class WinBasedAttention(nn.Module):
         three-launch path).  LIC_FUSED_WBA_PROJ=1 also folds the proj + shortcut into that launch
         (bit-identical, but slower today: DESIGN.md section 5)."""
         if _FUSED and Fn.wba_qkv_attn_ok(x, self.dim, self.num_heads, self.window_size):
-            fuse_proj = _FUSED_PROJ and not proj_kw and (out is None or out.t.data_ptr() != x.t.data_ptr())
+            # the fused proj stores 16 B per lane: only into a fresh buffer or a 16-B aligned view
+            # with 4-element rows, never onto x (the shortcut) -- else the proj runs as its own launch
+            fuse_proj = _FUSED_PROJ and not proj_kw and (
+                out is None or (out.t.data_ptr() != x.t.data_ptr() and out.ptr % 16 == 0 and out.ld % 4 == 0))
             a = Fn.wba_qkv_attn(x, self.attn.qkv.packed(x.dtype), self.num_heads, self.window_size, self.shift_size,
                                 self.attn.relative_position_bias_table, self.num_heads, 1,
                                 1 if self.shift_size > 0 else 0, float(self.attn.scale),

@@ -10,6 +10,9 @@ y - mu (or to sit next to an earlier near-tie flip: a flipped y_hat of slice i m
 the later slices in its window), and bounds the rate; with no near-ties the result is
 bit-exact (all 256^2 cases measure 0 flips).
 """
+import json
+import os
+
 import torch
 
 TIE_EPS = 2e-4      # |frac(y - mu) - 0.5| of a summation-order flip (measured <= 1e-4)
@@ -131,3 +134,30 @@ def check_decoder(last: dict, ref: dict, P: dict, flips: int, tol: float = 1e-4,
     assert _rel(last["x_tilde"], xt_ref) < tol
     d8 = (_u8(last["x_rec"]) - _u8(xr_ref)).abs()
     assert int(d8.max()) <= 1 and (d8 > 0).float().mean().item() < 1e-4
+
+
+def near_tie_count(sym_gpu: torch.Tensor, ref: dict) -> int:
+    """Flipped symbols whose oracle y - mu is a near-tie (|frac - 0.5| < TIE_EPS)."""
+    ne = sym_gpu.cpu() != ref["symbols"]
+    d = ref["z3"] - ref["means"]
+    dist = ((d - torch.floor(d)) - 0.5).abs()
+    return int((ne & (dist < TIE_EPS)).sum())
+
+
+def record(config: str, precision: str, **fields) -> None:
+    """Append one parity record (JSON line) to $LIC_PARITY_RECORD when set (the round's per-config
+    parity table, profiles/r05/parity_configs.jsonl)."""
+    path = os.environ.get("LIC_PARITY_RECORD")
+    if not path:
+        return
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "a") as f:
+        f.write(json.dumps(dict(config=config, precision=precision, **fields)) + "\n")
+
+
+def check_x6_rate_not_worse(d_bpp: dict) -> None:
+    """The headline's fp32x6 path may not drift further from the oracle's free-running rate than
+    max(1e-5, the exact-fp32 path's own drift) on the same batch (VERDICT r4 next #7)."""
+    if "fp32x6" in d_bpp and "fp32" in d_bpp:
+        assert d_bpp["fp32x6"] <= max(1e-5, d_bpp["fp32"]) + 1e-12, \
+            f"fp32x6 free-running d_bpp {d_bpp['fp32x6']:.3e} > max(1e-5, exact fp32 {d_bpp['fp32']:.3e})"

@@ -21,7 +21,8 @@ import pytest
 import torch
 
 from oracle import ref_cpu as R
-from parity import check_decoder, check_flip_sets_match, check_rate, check_symbols
+from parity import (check_decoder, check_flip_sets_match, check_rate, check_symbols, check_x6_rate_not_worse,
+                    near_tie_count, record)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -74,12 +75,15 @@ def _check_precision(arch, prec, B, S, net0, x, ref, P):
           f"{rate['d_bpp_same_symbols']:.2e}, per image max {rate['d_bpp_per_image']:.2e}; flip bits "
           f"{rate['flip_bits']:.2f}) d_psnr {abs(v_psnr.item() - ref['v_psnr'].item()):.2e} "
           f"(per flip-free image max {d_img.max().item() if d_img.numel() else 0.0:.2e}, {int(clean.sum())} images)")
+    record(f"{arch} B={B} {S}x{S}", prec, flips=flips, near_ties=near_tie_count(net.last["symbols"], ref),
+           d_bpp=rate["d_bpp"], d_bpp_same_symbols=rate["d_bpp_same_symbols"], flip_bits=rate["flip_bits"],
+           d_psnr_db=abs(v_psnr.item() - ref["v_psnr"].item()), symbols=int(ref["symbols"].numel()))
     assert abs(v_psnr.item() - ref["v_psnr"].item()) <= 1e-4
     assert d_img.numel() == 0 or d_img.max().item() <= 1e-4
     check_decoder(net.last, ref, P, flips)
     del net
     torch.cuda.empty_cache()
-    return flipped
+    return flipped, rate["d_bpp"]
 
 
 def _compare_forward(arch, B, S, seed, xseed, precisions=("fp32", "fp32x6")):
@@ -90,7 +94,9 @@ def _compare_forward(arch, B, S, seed, xseed, precisions=("fp32", "fp32x6")):
     P = {k: v.detach().float() for k, v in net0.state_dict().items()}
     x = _x(B, S, xseed)
     ref = R.net_forward(x, P, arch=arch)
-    masks = {p: _check_precision(arch, p, B, S, net0, x, ref, P) for p in precisions}
+    res = {p: _check_precision(arch, p, B, S, net0, x, ref, P) for p in precisions}
+    masks = {p: r[0] for p, r in res.items()}
+    check_x6_rate_not_worse({p: r[1] for p, r in res.items()})
     if "fp32" in masks and "fp32x6" in masks:
         n = check_flip_sets_match(masks["fp32x6"], masks["fp32"], ref)
         print(f"flip-set difference fp32x6 vs exact fp32: {n}")

@@ -1,0 +1,198 @@
+"""The round-5 16-bit convolution kernel (csrc/conv16.h: transposed MFMA, weights + halo by
+LDS-DMA, register epilogue) on the shapes it takes -- stride-1 3x3 / 7x7, >= 16 x 32-pixel maps,
+>= 128 tiles -- against torch fp32 on the CPU on the 16-bit-rounded operands (so the bar measures
+the kernel's fp32 accumulation and its one output rounding, not the input cast), and against the
+generic implicit-GEMM kernel.  Epilogue operand sets (none / r1 / gate g+r1+r2), ragged tiles,
+channel-window views and the second destination are covered.  Reference layers: the
+Win_noShift_Attention / ResidualBlock 3x3s and the 7x7 of /root/reference/layers/layers.py:87-102,
+the ResidualBottleneck 3x3 96->96 of /root/reference/model/net_ga.py:89-103."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+# fp16: one output rounding (2^-11 relative) + accumulation order; bf16: 2^-8 relative
+TOL = {torch.float16: 4e-3, torch.bfloat16: 1.2e-2}
+
+
+def _act(x, dtype):
+    from lic_amd.functional import Act
+    return Act.from_nchw(x.to(DEV).contiguous(), dtype)
+
+
+def _rounded(t, dtype):
+    return t.to(dtype).float()
+
+
+def _check(out, ref, dtype, what):
+    out = out.float().cpu()
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    print(f"\n[{what}] max err {err:.3e} (scale {scale:.2f})")
+    assert torch.isfinite(out).all()
+    assert err <= TOL[dtype] * scale, what
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,B,H,W", [
+    (192, 192, 3, 32, 64, 64),    # the bench's roofline shape (Win_noShift_Attention 3x3 @ H/4, B=32)
+    (192, 192, 3, 16, 64, 64),    # 128 tiles
+    (192, 192, 3, 4, 128, 128),   # ResidualBlockWithStride conv2 @ H/2
+    (192, 192, 7, 16, 64, 64),    # conv7x7 (tap-row groups)
+    (96, 96, 3, 32, 64, 64),      # ResidualBottleneck 3x3 96->96 (96-channel blocks)
+    (192, 192, 3, 12, 50, 70),    # ragged tiles in both directions (50 = 3*16+2, 70 = 2*32+6)
+    (192, 192, 7, 12, 40, 45),    # ragged 7x7
+])
+def test_conv16_vs_torch_fp32(dtype, cin, cout, k, B, H, W):
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(50 + k)
+    m = Conv2d(cin, cout, k, 1, k // 2)
+    x = torch.randn(B, cin, H, W) * 0.5
+    out = m.to(DEV).run(_act(x, dtype)).nchw()
+    ref = F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 1, k // 2)
+    _check(out, ref, dtype, f"conv{k}x{k} {cin}->{cout} {dtype} B={B} {H}x{W}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W", [(16, 128, 128), (16, 100, 134)])
+def test_conv16_stride2_phases_vs_torch_fp32(dtype, B, H, W):
+    """ZeroPad2d((1,2,1,2)) + conv5x5 s2 (net_ga.py:277-282): the four input-parity phases (3x3 / 3x2 /
+    2x3 / 2x2 taps) accumulate in registers; ragged output (50 x 67 from 100 x 134)."""
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(55)
+    m = Conv2d(192, 192, 5, 2, 0)
+    x = torch.randn(B, 192, H, W) * 0.5
+    out = m.to(DEV).run(_act(x, dtype), pad=(1, 1, 2, 2)).nchw()
+    ref = F.conv2d(F.pad(_rounded(x, dtype), (1, 2, 1, 2)), _rounded(m.weight.detach().cpu(), dtype),
+                   m.bias.detach().cpu(), 2)
+    _check(out, ref, dtype, f"ZeroPad+conv5x5 s2 {dtype} B={B} {H}x{W}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_conv16_matches_generic(dtype):
+    """conv16 vs the generic implicit-GEMM kernel on the same packed operands."""
+    from lic_amd.layers import Conv2d
+    import lic_amd.functional as Fn
+    torch.manual_seed(60)
+    m = Conv2d(192, 192, 3, 1, 0).to(DEV)
+    x = _act(torch.randn(16, 192, 64, 64), dtype)
+    pk = m.packed(dtype, (1, 1, 1, 1))
+    a = Fn.conv(x, pk).nchw().float()
+    b = Fn.conv(x, pk, force_generic=True).nchw().float()
+    scale = b.abs().max().item()
+    assert (a - b).abs().max().item() <= TOL[dtype] * scale
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_conv16_epilogues_views_dual_store(dtype):
+    """The epilogue operand sets the a_model uses on these convs (LeakyReLU; + residual; the
+    Win_noShift_Attention gate g*sigmoid(lrelu(acc+b) + r1) + r2), on channel-window views of
+    wider buffers, with a second destination."""
+    from lic_amd.layers import Conv2d
+    from lic_amd.functional import Act
+    from lic_amd import _ffi as L
+    torch.manual_seed(61)
+    B, H, W, C = 16, 64, 64, 192
+    m = Conv2d(C, C, 3, 1, 1).to(DEV)
+    big = (torch.randn(B, H, W, 3 * C + 64, device=DEV) * 0.5).to(dtype)
+    X, R1, G = Act(big, 64, C), Act(big, 64 + C, C), Act(big, 64 + 2 * C, C)
+    R2 = Act(big, 0, C)   # overlaps the first channels of X: a read-only view
+
+    def nchw(view):
+        return view.t[..., view.c0:view.c0 + view.c].float().permute(0, 3, 1, 2).cpu()
+
+    base = F.conv2d(nchw(X), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 1, 1)
+    cases = [
+        (dict(act=L.ACT_LRELU), F.leaky_relu(base)),
+        (dict(act=L.ACT_LRELU, r1=R1), F.leaky_relu(base) + nchw(R1)),
+        (dict(act=L.ACT_LRELU, r1=R1, epi=L.EPI_GATE, g=G, r2=R2),
+         nchw(G) * torch.sigmoid(F.leaky_relu(base) + nchw(R1)) + nchw(R2)),
+    ]
+    for idx, (kw, ref) in enumerate(cases):
+        out_buf = torch.zeros(B, H, W, C + 96, device=DEV, dtype=dtype)
+        out2 = torch.zeros(B, H, W, C + 32, device=DEV, dtype=dtype)
+        m.run(X, out=Act(out_buf, 96, C), y2=Act(out2, 0, C), **kw)
+        _check(out_buf[..., 96:].permute(0, 3, 1, 2), ref, dtype, f"epilogue case {idx} {dtype}")
+        assert torch.equal(out_buf[..., 96:], out2[..., :C])
+        assert out_buf[..., :96].abs().sum().item() == 0 and out2[..., C:].abs().sum().item() == 0
+
+
+# ---- gemm16 (csrc/gemm16.h): 16-bit 1x1 convolutions on maps of >= 16 K output pixels ----
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,s,B,H,W", [
+    (192, 576, 1, 32, 64, 64),   # WinBasedAttention qkv Linear (three 192-channel blocks)
+    (192, 192, 1, 16, 64, 64),   # proj / conv_b 1x1
+    (192, 96, 1, 16, 64, 64),    # ResidualBottleneck 192->96 (96-channel blocks)
+    (96, 192, 1, 16, 64, 64),    # ResidualBottleneck 96->192 (K = 96)
+    (192, 192, 2, 8, 128, 130),  # ResidualBlockWithStride 1x1 s2 skip, ragged (65 columns)
+    (192, 192, 1, 7, 50, 47),    # pixel count not a multiple of 32
+])
+def test_gemm16_vs_torch_fp32(dtype, cin, cout, s, B, H, W):
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(70 + cin + cout)
+    m = Conv2d(cin, cout, 1, s, 0)
+    x = torch.randn(B, cin, H, W) * 0.5
+    out = m.to(DEV).run(_act(x, dtype)).nchw()
+    ref = F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), s)
+    _check(out, ref, dtype, f"1x1 s{s} {cin}->{cout} {dtype} B={B} {H}x{W}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_gemm16_epilogues_views(dtype):
+    """LeakyReLU / GELU, + residual (the proj shortcut) on channel-window views with a second
+    destination."""
+    from lic_amd.layers import Conv2d
+    from lic_amd.functional import Act
+    from lic_amd import _ffi as L
+    torch.manual_seed(71)
+    B, H, W, C = 8, 64, 64, 192
+    m = Conv2d(C, C, 1, 1, 0).to(DEV)
+    big = (torch.randn(B, H, W, 2 * C + 32, device=DEV) * 0.5).to(dtype)
+    X, R1 = Act(big, 32, C), Act(big, 32 + C, C)
+
+    def nchw(view):
+        return view.t[..., view.c0:view.c0 + view.c].float().permute(0, 3, 1, 2).cpu()
+
+    base = F.conv2d(nchw(X), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu())
+    for idx, (kw, ref) in enumerate([(dict(act=L.ACT_GELU), F.gelu(base)),
+                                     (dict(r1=R1), base + nchw(R1)),
+                                     (dict(act=L.ACT_LRELU, r1=R1), F.leaky_relu(base) + nchw(R1))]):
+        out_buf = torch.zeros(B, H, W, C + 64, device=DEV, dtype=dtype)
+        out2 = torch.zeros(B, H, W, C, device=DEV, dtype=dtype)
+        m.run(X, out=Act(out_buf, 64, C), y2=Act(out2), **kw)
+        _check(out_buf[..., 64:].permute(0, 3, 1, 2), ref, dtype, f"1x1 epilogue case {idx} {dtype}")
+        assert torch.equal(out_buf[..., 64:], out2)
+        assert out_buf[..., :64].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("variant", ["compressai", "model_gdn", "model_igdn"])
+def test_gemm16_gdn(dtype, variant):
+    """GDN / IGDN at 128x128 (the a_model's GDN after ResidualBlockWithStride): x^2 prologue in
+    registers + the rsqrt / div / sqrt epilogue with g = x, vs the oracle restatement
+    (layers/gdn.py:62-75, model/gdn.py:69-92)."""
+    from oracle import ref_cpu as R
+    torch.manual_seed(72)
+    C = 192
+    if variant == "compressai":
+        from lic_amd.layers import GDN
+        m = GDN(C)
+    else:
+        from lic_amd.model.gdn import GDN, IGDN
+        m = IGDN(C, inverse=True) if variant == "model_igdn" else GDN(C)
+    with torch.no_grad():
+        m.beta.add_(0.3 * torch.rand(C))
+        m.gamma.add_(0.05 * torch.rand(C, C))
+    m = m.to(DEV)
+    x = torch.randn(2, C, 128, 96) * 2
+    out = m.run(_act(x, dtype)).nchw().float().cpu()
+    P = {"g." + k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+    xr = _rounded(x, dtype)
+    ref = R.gdn_compressai(xr, P, "g") if variant == "compressai" else R.gdn_model(xr, P, "g", inverse=(variant == "model_igdn"))
+    # the x^2 operand is rounded to the 16-bit type before the MFMA (as every 16-bit kernel does)
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= (1e-2 if dtype == torch.float16 else 3e-2) * scale, (variant, err, scale)

@@ -12,7 +12,8 @@ import pytest
 import torch
 
 from oracle import ref_cpu as R
-from parity import check_decoder, check_flip_sets_match, check_rate, check_symbols
+from parity import (check_decoder, check_flip_sets_match, check_rate, check_symbols, check_x6_rate_not_worse,
+                    near_tie_count, record)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -91,7 +92,7 @@ def test_net_fp32_parity_kodak_shape(arch, hw):
     H, W = hw
     mod = net_ga if arch == "net_ga" else net_unet_ha_hs
     x = eval_net.synthetic_image(4, H, W).unsqueeze(0) * 2 - 1
-    ref, P, masks = None, None, {}
+    ref, P, masks, d_bpp = None, None, {}, {}
     for prec in ("fp32", "fp32x6"):
         torch.manual_seed(2)
         net = net_ga.synthetic_syntax_bias_(mod.Net((1, H, W, 3), (1, H, W, 3), False, False, precision=prec), 2)
@@ -112,21 +113,36 @@ def test_net_fp32_parity_kodak_shape(arch, hw):
         print(f"\n[{arch} {H}x{W} {prec}] bpp gpu={bpp.item():.8f} ref={ref['bpp'].item():.8f} "
               f"psnr gpu={v_psnr.item():.6f} ref={ref['v_psnr'].item():.6f} flips {flips} "
               f"(d_bpp on the same symbols {rate['d_bpp_same_symbols']:.2e}, flip bits {rate['flip_bits']:.2f})")
+        record(f"{arch} B=1 {H}x{W} (config 4 shape)", prec, flips=flips,
+               near_ties=near_tie_count(net.last["symbols"], ref), d_bpp=rate["d_bpp"],
+               d_bpp_same_symbols=rate["d_bpp_same_symbols"], flip_bits=rate["flip_bits"],
+               d_psnr_db=abs(v_psnr.item() - ref["v_psnr"].item()), symbols=int(ref["symbols"].numel()))
+        d_bpp[prec] = rate["d_bpp"]
         assert abs(v_psnr.item() - ref["v_psnr"].item()) <= 1e-4
         check_decoder(net.last, ref, P, flips)
         del net
     check_flip_sets_match(masks["fp32x6"], masks["fp32"], ref)
+    check_x6_rate_not_worse(d_bpp)
 
 
 def test_rd_sweep_runs_two_lambdas():
-    """eval_net --synthetic-kodak: the config-4 sweep (2 lambdas, graph replay) on one GPU."""
+    """eval_net --synthetic-kodak: the config-4 sweep (2 lambdas, graph replay) on one GPU, batched per
+    image shape (the default) and one image per forward: the same per-image means."""
     import eval_net
-    summ, ips, world = eval_net.rd_sweep([0.0018, 0.0932], "", arch="net_ga", precision="fp16", graph=True)
-    assert world == 1 and len(summ) == 2 and all(s["images"] == 24 for s in summ)
-    assert all(math.isfinite(s["bpp"]) and s["bpp"] > 0 and math.isfinite(s["psnr"]) for s in summ)
-    assert ips > 0
-    print(f"\n[rd sweep] {ips:.1f} images/s; " + "; ".join(f"{s['lambda']}: {s['bpp']:.4f} bpp {s['psnr']:.3f} dB"
-                                                        for s in summ))
+    res = {}
+    for batched in (True, False):
+        summ, ips, world = eval_net.rd_sweep([0.0018, 0.0932], "", arch="net_ga", precision="fp32x6", graph=True,
+                                             batched=batched)
+        assert world == 1 and len(summ) == 2 and all(s["images"] == 24 for s in summ)
+        assert all(math.isfinite(s["bpp"]) and s["bpp"] > 0 and math.isfinite(s["psnr"]) for s in summ)
+        assert ips > 0
+        res[batched] = summ
+        print(f"\n[rd sweep fp32x6 {'batched' if batched else 'per image'}] {ips:.1f} images/s; " +
+              "; ".join(f"{s['lambda']}: {s['bpp']:.6f} bpp {s['psnr']:.5f} dB" for s in summ))
+    for a, b in zip(res[True], res[False]):
+        # per-image means of the same images; only fp32 summation order differs (batch-size-dependent
+        # tiles): the bar is the north-star one
+        assert abs(a["bpp"] - b["bpp"]) <= 1e-5 and abs(a["psnr"] - b["psnr"]) <= 1e-4, (a, b)
 
 
 @pytest.mark.parametrize("arch", ["net_ga", "net_unet_ha_hs"])

@@ -11,8 +11,10 @@ Differences:
     net the script's name refers to) or net_ga (eval_net.py's model): the reference script's
     ``model/Net_unet.py`` imports the missing ``model/Block.py`` and cannot be built;
   * one process per GPU (``torch.distributed.run``) with a bucketed gradient all-reduce
-    overlapped with the backward (lic_amd.distributed.GradAllReduce, RCCL over xGMI)
-    instead of single-process ``nn.DataParallel`` (:152);
+    (lic_amd.distributed.GradAllReduce, RCCL over xGMI) instead of single-process
+    ``nn.DataParallel`` (:152): eager steps launch each bucket from a post-accumulate-grad hook
+    while the backward continues; a captured step (``--graph``, opt-in at world > 1) launches all
+    buckets after the backward (DESIGN.md section 9, serialised cost);
   * data: no DIV2K and no network here — ``--synthetic`` (default) draws random 256x256
     crops from a seeded bank of smooth synthetic images resident in HBM;
   * ``--precision bf16`` (default, BASELINE config 5): bf16 activations / MFMA operands
@@ -98,12 +100,12 @@ def main():
     rank, world, local = D.init("nccl")
     if D.launched() and args.gpus > 1 and world != args.gpus:
         raise SystemExit(f"train_net_unet.py: --gpus {args.gpus} but the launcher started {world} ranks")
-    # bf16 / fp32: the captured step is the default, on one GPU and on N (the bucketed RCCL gradient
-    # all-reduce is captured with the backward; replays equal the eager steps,
-    # tests/test_gpu_train_net.py::test_train_step_hipgraph_matches_eager,
-    # tests/test_gpu_dist_train.py::test_graph_step_with_rccl_allreduce_matches_eager); ~7000 launches
-    # per step otherwise leave the GPU waiting on the host
-    args.graph = not args.eager and (args.graph or args.precision != "fp16")
+    # bf16 / fp32 on ONE GPU: the captured step is the default (replays equal the eager steps,
+    # tests/test_gpu_train_net.py::test_train_step_hipgraph_matches_eager; ~7000 launches per step
+    # otherwise leave the GPU waiting on the host).  At world > 1 it is opt-in (--graph): the captured
+    # RCCL all-reduce is tested on one rank only (test_gpu_dist_train.py), no multi-rank captured step
+    # has run yet
+    args.graph = not args.eager and (args.graph or (world == 1 and args.precision != "fp16"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B = int(args.batch_size)
