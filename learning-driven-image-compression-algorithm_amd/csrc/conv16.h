@@ -34,6 +34,14 @@ typedef __attribute__((address_space(3))) void c16_lds_void;
 #ifndef C16_STAMP
 #define C16_STAMP 0
 #endif
+// diagnostic ablations (-DC16_ABL=bits, timing only, outputs wrong): 1 no stores in the register epilogue
+#ifndef C16_ABL
+#define C16_ABL 0
+#endif
+// a stage's LDS-DMA pieces are issued over its first C16_ISSUE taps
+#ifndef C16_ISSUE
+#define C16_ISSUE 6
+#endif
 #if C16_STAMP
 #define C16T(v)                                                                          \
   do {                                                                                   \
@@ -56,6 +64,35 @@ __device__ __forceinline__ void c16_static_for(F&& f) {
   }
 }
 
+// The epilogue variants the conv16 / gemm16 launches take (lic_common.h epilogue_run on NQ staged
+// 32 x 32 tiles, ct + q * 32 * 33): plain, + r1, gate (g, r1, r2), GDN (g), and the scalar path
+// (unaligned views, pixel shuffle).  Fewer compiled variants than epilogue_all's seven.
+inline int c16_epi_mask_host(const lic_conv_args& a) {
+  const bool gdn = a.epi == LIC_EPI_GDN_DIV || a.epi == LIC_EPI_GDN_RSQRT || a.epi == LIC_EPI_GDN_SQRT;
+  return ((gdn || a.epi == LIC_EPI_GATE) ? EPI_G : 0) | ((a.r1 != nullptr && a.epi != LIC_EPI_HALF_TANH) ? EPI_R1 : 0) |
+         ((a.epi == LIC_EPI_HALF_TANH || a.epi == LIC_EPI_GATE) ? EPI_R2 : 0);   // = epi_mask()
+}
+inline bool c16_epi_supported(const lic_conv_args& a) {
+  const int m = c16_epi_mask_host(a);
+  return m == 0 || m == EPI_R1 || m == EPI_G || m == (EPI_G | EPI_R1 | EPI_R2);
+}
+template <typename T, int NQ, int TN, int CT_STRIDE, typename Stage>
+__device__ __forceinline__ void c16_epilogue(const lic_conv_args& a, float* ct, const int* rowpix, int n0,
+                                             const float* sbias, int lane, Stage& stage) {
+  if (!epi_vec_ok<T>(a)) {
+    epilogue_run<T, NQ, TN, -1, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
+    return;
+  }
+  switch (epi_mask(a)) {
+    case 0: epilogue_run<T, NQ, TN, 0, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage); break;
+    case EPI_R1: epilogue_run<T, NQ, TN, EPI_R1, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage); break;
+    case EPI_G: epilogue_run<T, NQ, TN, EPI_G, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage); break;
+    default:
+      epilogue_run<T, NQ, TN, EPI_G | EPI_R1 | EPI_R2, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
+      break;
+  }
+}
+
 // One LDS-DMA piece: 64 lanes x 16 B from rsrc + voffset + soffset to lds + 16 * lane.  (In a
 // __device__ helper: used directly in the kernel body, the builtin makes the host pass drop the
 // kernel's launch stub.)
@@ -70,6 +107,7 @@ struct C16Plan {
   unsigned xrec;      // bytes addressable from a.x (buffer range; past it loads read zeros)
   unsigned wrec;      // bytes of the packed weights
   int nst;            // stages = nchunks * ngroups
+  int fast_epi;       // 1: the register epilogue applies (c16_fast_epi_ok)
 };
 
 // S = 1: stages are (chunk, group of G taps = G/KW tap rows).  S = 2: stages are (chunk, input-parity
@@ -95,7 +133,7 @@ struct C16Geo {
   static constexpr int HPW = (HPIECES + NW - 1) / NW;   // halo pieces per wave (max)
   static constexpr int WPW = (WPIECES + NW - 1) / NW;   // weight pieces per wave (max)
   static constexpr int LDS_PIPE = 2 * HBYTES + 2 * WBYTES;          // the main loop's double buffers
-  static constexpr int LDS_EPI = NW * CT * 32 * 33 * 4;               // the epilogue's per-wave slots
+  static constexpr int LDS_EPI = NW * 32 * 33 * 4;                    // the epilogue's per-wave slots (>= 32 x 80 B)
   static constexpr int LDS_MAIN = LDS_PIPE > LDS_EPI ? LDS_PIPE : LDS_EPI;
   static constexpr int SMEM = LDS_MAIN + BN * 4 + TH * TW * 4;     // + bias + destination pixels
   static_assert(S == 2 || (NTAPS % G == 0 && G % KW == 0), "a tap group is whole tap rows");
@@ -103,7 +141,7 @@ struct C16Geo {
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
-template <typename T, int KH, int KW, int S, int G, int BN, int WN>
+template <typename T, int KH, int KW, int S, int G, int BN, int WN, bool FAST>
 __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, const C16Plan p) {
   using Geo = C16Geo<KH, KW, S, G, BN, WN>;
   constexpr int NW = Geo::NW, PJ = Geo::PJ, CT = Geo::CT, HWD = Geo::HWD;
@@ -248,7 +286,7 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
     constexpr int NTX = S == 1 ? KW : (PH & 1 ? KW / 2 : (KW + 1) / 2);
     constexpr int NTP = NTY * NTX;
     // pieces are issued during the first ISSUE taps of a stage (the rest of the stage hides them)
-    constexpr int ISSUE = NTP < 6 ? NTP : 6;
+    constexpr int ISSUE = NTP < C16_ISSUE ? NTP : C16_ISSUE;
     const char* hrow = hbuf + (S == 1 ? (g * G) / KW : 0) * HWD * 32;
     auto load_a = [&](int tt, u32x4(&fa)[CT]) {
 #pragma unroll
@@ -307,18 +345,89 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
   // accumulators hold 4-channel runs; stored as they are, every store would touch 32 cache lines) ----
   // one pass per tile row: its CT tiles are staged first (their accumulators die before the operand
   // loads of the pass), then finished
-  float* ct = (float*)smem + wave * (CT * 32 * 33);
-  c16_static_for<0, PJ>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
+  float* ct = (float*)smem + wave * (32 * 33);
+  // All CT * PJ tiles go through ONE runtime loop (epilogue_run, two tiles per iteration, operands one
+  // tile ahead) that stages tile q in the wave's slot by compile-time indices under a uniform test: the
+  // loop body runs from the instruction cache.  Unrolled per tile, the epilogue was ~250 k instructions
+  // of straight-line code, each executed once: 45 % of the kernel's cycles (stamps, profiles/r05).
+  auto stage_tile = [&](int q) {
+    c16_static_for<0, CT * PJ>([&](auto qc) {
+      constexpr int qq = decltype(qc)::value;
+      if (q == qq) {
 #pragma unroll
-    for (int i = 0; i < CT; ++i)
+        for (int r = 0; r < 16; ++r) ct[l32 * 33 + 8 * (r >> 2) + 4 * lh + (r & 3)] = acc[qq % CT][qq / CT][r];
+      }
+    });
+  };
+  if constexpr (FAST) {
+    // Register epilogue (plain / + residual with a cheap activation, 16-B aligned views, whole
+    // channel tiles): bias + activation (+ r1) on the accumulators as they stand (4-channel runs of
+    // one pixel per lane), rounded, staged as 16-bit [pixel][channel] rows in the wave's slot, read
+    // back as 16 B of consecutive channels per lane and stored.  Unrolled per tile with compile-time
+    // accumulator indices and ~50 instructions a tile (the general epilogue spends ~250 a tile).
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    char* stg = smem + wave * (32 * 80);   // 32 rows of 64 B, padded to 80 B (conflict-free b64 writes)
+    T* __restrict__ yg = (T*)a.y;
+    T* __restrict__ y2g = (T*)a.y2;
+    const T* __restrict__ r1g = (const T*)a.r1;
+    const int act = a.act;
+    const float slope = a.slope;
+    c16_static_for<0, CT * PJ>([&](auto qc) {
+      constexpr int q = decltype(qc)::value, i = q % CT, j = q / CT;
+      const int row = i0 + wr * PJ + j;
+      const int nloc = wc * Geo::WCH + i * 32;       // channel of the tile's first column, in the block
+      // residual operand, in the accumulator layout (8 B = 4 channels per lane and run)
+      u32x2 rr[4];
+      if (r1g) {
+        const int col = j0 + l32;
+        const bool ok = row < a.mi && col < a.mj;
+        const int64_t pix = ok ? ((int64_t)b * a.ho + a.oy0 + a.osy * row) * a.wo + a.ox0 + a.osx * col : 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ct[i * 32 * 33 + l32 * 33 + 8 * (r >> 2) + 4 * lh + (r & 3)] = acc[i][j][r];
-    wave_lds_sync();
-    epilogue_all<T, CT, CT, void (*)(int), 32 * 33>(a, ct, rowpix + (wr * PJ + j) * 32, n0 + wc * Geo::WCH,
-                                                    sbias + wc * Geo::WCH, lane, [](int) {});
-    wave_lds_sync();
-  });
+        for (int k = 0; k < 4; ++k) rr[k] = *(const u32x2*)(r1g + pix * a.ldr1 + n0 + nloc + 8 * k + 4 * lh);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const floatx4 bv = *(const floatx4*)(sbias + nloc + 8 * k + 4 * lh);
+        float w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = acc[i][j][4 * k + e] + bv[e];
+        if (act == LIC_ACT_LRELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : w[e] * slope;
+        } else if (act == LIC_ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : 0.f;
+        }
+        if (r1g) {
+          const T* re = (const T*)&rr[k];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] += to_f(re[e]);
+        }
+        u32x2 raw;
+        T* o = (T*)&raw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = from_f<T>(w[e]);
+        *(u32x2*)(stg + l32 * 80 + (8 * k + 4 * lh) * 2) = raw;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int idx = lane + 64 * h, pr = idx >> 2, c4 = idx & 3;   // pixel of the tile row, 16-B chunk
+        const u32x4 val = *(const u32x4*)(stg + pr * 80 + c4 * 16);
+        const int col = j0 + pr;
+        if (row < a.mi && col < a.mj && !(C16_ABL & 1)) {
+          const int64_t pix = ((int64_t)b * a.ho + a.oy0 + a.osy * row) * a.wo + a.ox0 + a.osx * col;
+          const int n = n0 + nloc + c4 * 8;
+          *(u32x4*)(yg + pix * a.ldy + n) = val;
+          if (y2g) *(u32x4*)(y2g + pix * a.ldy2 + n) = val;
+        }
+      }
+      wave_lds_sync();
+    });
+  } else {
+    c16_epilogue<T, CT * PJ, CT, 0>(a, ct, rowpix + wr * PJ * 32, n0 + wc * Geo::WCH, sbias + wc * Geo::WCH, lane,
+                                    stage_tile);
+  }
 #if C16_STAMP
   C16T(t_end);
   if (tid == 0) {
@@ -334,12 +443,22 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
 #endif
 }
 
+// The register epilogue: plain or + r1 (PLAIN), activation none / relu / lrelu (GELU's erf would bloat it),
+// every view 16-B aligned with rows of whole 16-B chunks, whole 32-channel tiles, no pixel shuffle.
+inline bool c16_fast_epi_ok(const lic_conv_args& a, int esz) {
+  auto al = [&](const void* ptr, int ld) { return ptr == nullptr || (((uintptr_t)ptr & 15) == 0 && (ld * esz) % 16 == 0); };
+  const int m = c16_epi_mask_host(a);
+  return (m == 0 || m == EPI_R1) && a.epi == LIC_EPI_PLAIN && a.out_shuffle == 0 && a.co == a.copad &&
+         (a.act == LIC_ACT_NONE || a.act == LIC_ACT_RELU || a.act == LIC_ACT_LRELU) &&
+         al(a.y, a.ldy) && al(a.y2, a.ldy2) && (a.r1 == nullptr || (((uintptr_t)a.r1 & 7) == 0 && a.ldr1 % 4 == 0));
+}
+
 // Returns 1 and launches when the conv16 kernel applies; 0 to let the caller fall back.
 template <typename T, int KH, int KW, int S, int G, int BN, int WN>
 int try_conv16(const lic_conv_args& a, hipStream_t s, int& status) {
   using Geo = C16Geo<KH, KW, S, G, BN, WN>;
   if (a.ntaps != KH * KW || a.copad % BN || a.isy != S || a.isx != S) return 0;
-  if (a.prologue != LIC_PRO_NONE || a.groups != 1) return 0;
+  if (a.prologue != LIC_PRO_NONE || a.groups != 1 || !c16_epi_supported(a)) return 0;
   if (a.ci != a.cpad || a.cpad % 16 || a.ldx % 8 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt % 16)) return 0;
   // unit-spaced tap grid KH x KW in row-major order
   for (int t = 0; t < a.ntaps; ++t)
@@ -356,9 +475,10 @@ int try_conv16(const lic_conv_args& a, hipStream_t s, int& status) {
   p.xrec = (unsigned)xbytes;
   p.wrec = (unsigned)wbytes;
   p.nst = p.nchunks * Geo::NG;
+  p.fast_epi = c16_fast_epi_ok(a, 2) && wd_env("LIC_C16_FAST_EPI", 1) ? 1 : 0;
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   dim3 grid((unsigned)blocks, a.copad / BN);
-  auto kern = conv16_kernel<T, KH, KW, S, G, BN, WN>;
+  auto kern = p.fast_epi ? conv16_kernel<T, KH, KW, S, G, BN, WN, true> : conv16_kernel<T, KH, KW, S, G, BN, WN, false>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, Geo::SMEM);
   if (ea != hipSuccess) {
     status = fail(std::string("conv16: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -383,8 +503,8 @@ int conv16_dispatch_impl(const lic_conv_args& a, hipStream_t s, int& status) {
       if (a.copad % 192 == 0 && blocks(192) >= 128) return try_conv16<T, 3, 3, 1, 9, 192, 2>(a, s, status);
       if (a.copad % 96 == 0 && blocks(96) >= 128) return try_conv16<T, 3, 3, 1, 9, 96, 1>(a, s, status);
     }
-    if (a.ntaps == 49 && a.copad % 192 == 0 && blocks(192) >= 128)
-      return try_conv16<T, 7, 7, 1, 7, 192, 2>(a, s, status);
+    // (7x7 stays on the halo kernel: the 7 tap-column bases next to 12 accumulator tiles and the
+    // epilogue's operand sets spilled 536 VGPRs, 1.9 ms against 0.40)
   }
   // ZeroPad2d((1,2,1,2)) + conv5x5 s2 (the a_model's downsampling convs): four input-parity phases
   if (a.isy == 2 && a.isx == 2 && a.ntaps == 25 && a.copad % 192 == 0 && blocks(192) >= 128 &&

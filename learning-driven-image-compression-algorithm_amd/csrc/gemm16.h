@@ -14,11 +14,10 @@
 //     32 x 32 tile in a wave-private LDS slot and stores 16 B of consecutive channels per lane.
 // MFMA is a quarter busy at the HBM rate: the bound is the bytes (x once, y once per N block).
 #pragma once
-#include "lic_common.h"
+#include "conv16.h"
 
 namespace lic {
 
-int wd_env(const char* name, int def);   // conv_split_wd.hip
 
 struct G16Plan {
   int M;          // output lattice pixels (n * mi * mj)
@@ -26,6 +25,7 @@ struct G16Plan {
   int nblk;       // output-channel blocks (copad / BN)
   int wgs;        // workgroups per channel block
   unsigned xrec;  // bytes addressable from a.x
+  unsigned wrec;  // bytes of the packed weights
 };
 
 template <typename T, int BN, int KST, int PRO>
@@ -47,17 +47,20 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
   const int rank = blockIdx.x / p.nblk;
   const int n0 = nb * BN;
 
-  // ---- weights of this channel block into LDS, once: slot (kk, n, stored half ph) holds channel
-  // half ph ^ bit3(n) of K step kk ----
+  // ---- weights of this channel block into LDS, once, by LDS-DMA (all pieces in flight together):
+  // slot (kk, n, stored half ph) holds channel half ph ^ bit3(n) of K step kk; a 1-KB piece is 32
+  // channels x 2 halves of one K step ----
   {
-    const T* __restrict__ wg = (const T*)a.wgt;
-    for (int sidx = tid; sidx < KST * BN * 2; sidx += NW * 64) {
-      const int kk = sidx / (BN * 2), rem = sidx - kk * BN * 2;
-      const int n = rem >> 1, ph = rem & 1;
-      const int c = ph ^ ((n >> 3) & 1);
-      *(u32x4*)(smem + sidx * 16) = *(const u32x4*)(wg + (int64_t)(n0 + n) * a.cpad + kk * 16 + c * 8);
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, (short)0, (int)p.wrec, 0x00020000);
+    const unsigned woff_lane = (unsigned)(((lane >> 1) * a.cpad + (((lane & 1) ^ ((lane >> 4) & 1)) * 8)) * 2);
+    constexpr int NPIECE = KST * BN / 32;
+    for (int P = wave; P < NPIECE; P += NW) {
+      const int kk = P / (BN / 32), nq = P - kk * (BN / 32);
+      c16_dma(wrs, smem + P * 1024, woff_lane, ((n0 + nq * 32) * a.cpad + kk * 16) * 2);
     }
     for (int n = tid; n < BN; n += NW * 64) sbias[n] = (a.bias && n0 + n < a.co) ? a.bias[n0 + n] : 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 
@@ -136,14 +139,16 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
     wave_lds_sync();
     // epilogue (lic_common.h): stage each 32x32 tile as [pixel][channel] in the wave's slot, finish it
     // with 16-B stores of consecutive channels
-    epilogue_all<T, TN, TN>(a, ct, rowpix, n0 + wc * 96, sbias + wc * 96, lane, [&](int q) {
+    // one wave-private slot, tile by tile (stage(q) writes tile q as [pixel][channel])
+    auto stage = [&](int q) {
 #pragma unroll
       for (int qq = 0; qq < TN; ++qq)
         if (qq == q) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) ct[l32 * 33 + 8 * (r >> 2) + 4 * lh + (r & 3)] = acc[qq][r];
         }
-    });
+    };
+    c16_epilogue<T, TN, TN, 0>(a, ct, rowpix, n0 + wc * 96, sbias + wc * 96, lane, stage);
     t = tn;
   }
 }
@@ -164,7 +169,7 @@ void launch_g16(const lic_conv_args& a, const G16Plan& p, dim3 grid, int smem, h
 template <typename T, int BN, int KST>
 int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
   if (a.ntaps != 1 || a.copad % BN || a.out_shuffle != 0 || a.groups != 1) return 0;
-  if (a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE) return 0;
+  if ((a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE) || !c16_epi_supported(a)) return 0;
   if (a.cpad != KST * 16 || a.ci != a.cpad || a.ldx % 8 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt % 16)) return 0;
   const int64_t xbytes = ((int64_t)a.n * a.h * a.w - 1) * a.ldx * 2 + (int64_t)a.ci * 2;
   const int64_t M = (int64_t)a.n * a.mi * a.mj;
@@ -179,6 +184,7 @@ int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
   if (wgs > need) wgs = need;
   p.wgs = wgs;
   p.xrec = (unsigned)xbytes;
+  p.wrec = (unsigned)((int64_t)a.copad * a.cpad * 2);
   const int smem = KST * BN * 32 + BN * 4 + 8 * 32 * 33 * 4 + 8 * 32 * 4;
   dim3 grid((unsigned)(wgs * p.nblk));
   if (a.prologue == LIC_PRO_SQUARE) launch_g16<T, BN, KST, LIC_PRO_SQUARE>(a, p, grid, smem, s, status);
