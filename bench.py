@@ -49,12 +49,18 @@ def _env_int(k, d):
         return d
 
 
-PMC_FILES = {torch.float16: "profiles/r02/pmc_conv3x3_64_f16.json",
+PMC_FILES = {torch.float16: "profiles/r05/pmc_conv3x3_64_f16.json",
              torch.float32: "profiles/r02/pmc_conv3x3_64_f32.json",
              ("split", 1): "profiles/r02/pmc_conv3x3_64_f32x3.json",
              ("split", 2): "profiles/r04/pmc_conv3x3_64_f32x6.json"}
 # the kernel that runs the roofline conv per precision (csrc/)
 ROOF_KERNEL = {0: "conv_halo_kernel", 1: "conv_halo_split_kernel", 2: "conv_split_wd_kernel"}
+# 16-bit activations run the roofline conv on csrc/conv16.h (round 5)
+ROOF_KERNEL_16 = "conv16_kernel"
+
+
+def _roof_kernel(dtype, split):
+    return ROOF_KERNEL_16 if (not split and dtype != torch.float32) else ROOF_KERNEL[split]
 # Net precision -> lic_conv_args.mfma_mode (lic_amd.functional.SPLIT_MODES)
 SPLIT_MODES = {"fp32x3": 1, "fp32x6": 2}
 # per split mode: 16-bit MFMA products per fp32 product, label
@@ -311,7 +317,8 @@ def extra_leg(args, other, x, device, gf_a):
            "a_model": {"ms": round(ta2 * 1e3, 3), "tflops": round(a2, 2), "frac_of_peak": round(a2 / peak2, 4)},
            "roofline": {"achieved": round(f2 / tk2 / 1e12, 2), "peak": peak2,
                         "frac": round(f2 / tk2 / 1e12 / peak2, 4),
-                        "traffic": _pmc_traffic(("split", split) if split else odt, args.batch, args.size)}}
+                        "traffic": _pmc_traffic(("split", split) if split else odt, args.batch, args.size),
+                        "kernel": _roof_kernel(odt, split)}}
     if other == "fp16":
         leg["note"] = ("fp16 activations (fp32 accumulation): NOT parity grade -- reported for the fp16-roofline "
                        "target")
@@ -454,7 +461,7 @@ def main():
                        "parallelism": f"image-sharded x{world} (independent batches, no collective)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": _pmc_traffic(("split", split) if split else dtype, args.batch, args.size),
-                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} ({ROOF_KERNEL[split]} {dname}), "
+                         "kernel": f"conv3x3 192->192 s1 @64x64 x{args.batch} ({_roof_kernel(dtype, split)} {dname}), "
                                    f"{flops / 1e9:.1f} GFLOP/launch, {tk * 1e6:.1f} us/launch",
                          "peak_note": (f"16-bit dense MFMA / {SPLIT_PRODUCTS[split]} (each fp32 product = "
                                        f"{SPLIT_PRODUCTS[split]} 16-bit MFMA products, csrc/conv_split.h)"

@@ -38,10 +38,11 @@ template <typename T> int gemm16_dispatch(const lic_conv_args& a, hipStream_t s,
 template <typename T>
 static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status) {
   if constexpr (sizeof(T) == 2) {   // round-5 16-bit kernels first
-    if (a.ntaps == 1) {
+    if (a.ntaps == 1 || a.ci <= 16) {
       if (int r = gemm16_dispatch<T>(a, s, status)) return r;
-    } else if (int r = conv16_dispatch<T>(a, s, status)) {
-      return r;
+    }
+    if (a.ntaps > 1) {
+      if (int r = conv16_dispatch<T>(a, s, status)) return r;
     }
   }
   const bool gemm_ok = a.ntaps == 1 && (HALO_1X1 == 2 || (HALO_1X1 == 1 && sizeof(T) == 4));

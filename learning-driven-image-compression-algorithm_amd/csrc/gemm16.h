@@ -19,6 +19,9 @@
 namespace lic {
 
 
+// a wave's epilogue slot: 32 x 33 fp32 (general) or 32 rows of 208 B + 32 destinations (register path)
+constexpr int G16_SLOT = 32 * 208 + 32 * 8;
+
 struct G16Plan {
   int M;          // output lattice pixels (n * mi * mj)
   int ntiles;     // ceil(M / 32)
@@ -26,9 +29,14 @@ struct G16Plan {
   int wgs;        // workgroups per channel block
   unsigned xrec;  // bytes addressable from a.x
   unsigned wrec;  // bytes of the packed weights
+  int fast_epi;   // 1: the register epilogue (g16_fast_epi_ok)
 };
 
-template <typename T, int BN, int KST, int PRO>
+// KT = 1: a 1x1 convolution, K step kk = input channels 16kk .. 16kk+15.  KT > 1: a small-Cin k x k
+// convolution (the image's first layers: Cin 8 or 16, any stride) as an implicit GEMM without a halo:
+// K step kk = tap kk's 16 channels, each lane loading its pixel's tap directly (the taps' re-reads of
+// neighbouring pixels are L1 / L2 hits); channels 8..15 read zeros when Cin is 8.
+template <typename T, int BN, int KST, int PRO, int KT = 1, bool FAST = false>
 __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, const G16Plan p) {
   // a wave computes 32 pixels x 96 channels (3 accumulator tiles); at BN = 192 two waves share each
   // pixel tile (its fragments are loaded twice, from L2 the second time)
@@ -36,8 +44,8 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
   static_assert(BN == 96 || BN == 192, "BN");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   float* sbias = (float*)(smem + KST * BN * 32);
-  float* cts = sbias + BN;                 // NW epilogue slots of 32 x 33 fp32
-  int* rowpix_all = (int*)(cts + NW * 32 * 33);   // NW x 32 destination pixels
+  float* cts = sbias + BN;                 // NW epilogue slots (G16_SLOT bytes)
+  int* rowpix_all = (int*)((char*)cts + NW * G16_SLOT);   // NW x 32 destination pixels
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -53,11 +61,12 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
   {
     const __amdgpu_buffer_rsrc_t wrs =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, (short)0, (int)p.wrec, 0x00020000);
-    const unsigned woff_lane = (unsigned)(((lane >> 1) * a.cpad + (((lane & 1) ^ ((lane >> 4) & 1)) * 8)) * 2);
+    const int wrow = a.ntaps * a.cpad;   // one output channel's packed weights [ntaps][cpad]
+    const unsigned woff_lane = (unsigned)(((lane >> 1) * wrow + (((lane & 1) ^ ((lane >> 4) & 1)) * 8)) * 2);
     constexpr int NPIECE = KST * BN / 32;
     for (int P = wave; P < NPIECE; P += NW) {
       const int kk = P / (BN / 32), nq = P - kk * (BN / 32);
-      c16_dma(wrs, smem + P * 1024, woff_lane, ((n0 + nq * 32) * a.cpad + kk * 16) * 2);
+      c16_dma(wrs, smem + P * 1024, woff_lane, ((n0 + nq * 32) * wrow + (KT == 1 ? kk * 16 : kk * a.cpad)) * 2);
     }
     for (int n = tid; n < BN; n += NW * 64) sbias[n] = (a.bias && n0 + n < a.co) ? a.bias[n0 + n] : 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -69,20 +78,38 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
   const int dy0 = a.dy[0], dx0 = a.dx[0];
   // weight fragment: row n = j*32 + l32, logical half lh
   const int wlane = l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) << 4) + wc * 96 * 32;
-  float* ct = cts + wave * 32 * 33;
+  float* ct = (float*)((char*)cts + wave * G16_SLOT);
   int* rowpix = rowpix_all + wave * 32;
 
   auto load_tile = [&](int t, u32x4(&xf)[KST]) __attribute__((always_inline)) {
     const int m = t * 32 + l32;
-    unsigned vo = 0x80000000u;   // past the map: out-of-range offsets read zeros
-    if (m < p.M) {
-      const int b = m / mij, rem = m - b * mij;
-      const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
-      const int iy = i * a.isy + dy0, ix = j * a.isx + dx0;
-      vo = (unsigned)((((int64_t)(b * a.h + iy) * a.w + ix) * a.ldx + lh * 8) * 2);
-    }
+    if constexpr (KT == 1) {
+      unsigned vo = 0x80000000u;   // past the map: out-of-range offsets read zeros
+      if (m < p.M) {
+        const int b = m / mij, rem = m - b * mij;
+        const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
+        const int iy = i * a.isy + dy0, ix = j * a.isx + dx0;
+        vo = (unsigned)((((int64_t)(b * a.h + iy) * a.w + ix) * a.ldx + lh * 8) * 2);
+      }
 #pragma unroll
-    for (int kk = 0; kk < KST; ++kk) xf[kk] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, kk * 32, 0);
+      for (int kk = 0; kk < KST; ++kk) xf[kk] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, kk * 32, 0);
+    } else {
+      int b = 0, iy0 = -(1 << 20), ix0 = 0;   // past the map: every tap out of the image
+      if (m < p.M && lh * 8 < a.ci) {
+        b = m / mij;
+        const int rem = m - b * mij;
+        const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
+        iy0 = i * a.isy;
+        ix0 = j * a.isx;
+      }
+#pragma unroll
+      for (int kk = 0; kk < KST; ++kk) {
+        const int iy = iy0 + a.dy[kk], ix = ix0 + a.dx[kk];
+        const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+        const unsigned vo = ok ? (unsigned)((((int64_t)(b * a.h + iy) * a.w + ix) * a.ldx + lh * 8) * 2) : 0x80000000u;
+        xf[kk] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0);
+      }
+    }
   };
 
   // each wave walks its own tiles with one register set: the next tile's loads are issued as soon as
@@ -122,55 +149,151 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
     }
     const int tn = __builtin_amdgcn_readfirstlane(t + stride);
     if (tn < p.ntiles) load_tile(tn, xc);
-    // destination pixels of the tile's 32 rows (wave-private; the previous tile's epilogue has
-    // finished reading them: LDS requests of a wave complete in order)
-    if (lh == 0) {
-      const int m = t * 32 + l32;
-      int base = -1;
-      if (m < p.M) {
+    const int m = t * 32 + l32;
+    if constexpr (FAST) {
+      // Register epilogue: bias, activation, GDN (g = the layer's input at the pixel) and residual on
+      // the accumulators as they stand (lane = pixel, 4-channel runs), rounded, staged as 16-bit
+      // [pixel][96 channels] rows (208-B pitch) in the wave's slot, stored as 16 B of consecutive
+      // channels per lane (six 1-KB stores per tile).  ~40 instructions per 32 x 32 tile against
+      // ~250 for lic_common.h's epilogue_run.
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      char* stg = (char*)ct;
+      const bool pok = m < p.M;
+      int64_t pix = 0;
+      if (pok) {
         const int b = m / mij, rem = m - b * mij;
         const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
-        int oy = a.oy0 + a.osy * i, ox = a.ox0 + a.osx * j;
-        if (a.out_shuffle >= 2) { oy *= 2; ox *= 2; }
-        base = (b * a.ho + oy) * a.wo + ox;
+        pix = ((int64_t)b * a.ho + a.oy0 + a.osy * i) * a.wo + a.ox0 + a.osx * j;
       }
-      rowpix[l32] = base;
-    }
-    wave_lds_sync();
-    // epilogue (lic_common.h): stage each 32x32 tile as [pixel][channel] in the wave's slot, finish it
-    // with 16-B stores of consecutive channels
-    // one wave-private slot, tile by tile (stage(q) writes tile q as [pixel][channel])
-    auto stage = [&](int q) {
+      const int nw = n0 + wc * 96;
+      const T* __restrict__ gg = (const T*)a.g;
+      const T* __restrict__ r1g = (const T*)a.r1;
+      const int epi = a.epi, act = a.act;
 #pragma unroll
-      for (int qq = 0; qq < TN; ++qq)
-        if (qq == q) {
+      for (int j = 0; j < TN; ++j) {
+        u32x2 og[4], o1[4];
 #pragma unroll
-          for (int r = 0; r < 16; ++r) ct[l32 * 33 + 8 * (r >> 2) + 4 * lh + (r & 3)] = acc[qq][r];
+        for (int k = 0; k < 4; ++k) {
+          const int n = nw + j * 32 + 8 * k + 4 * lh;
+          if (gg) og[k] = *(const u32x2*)(gg + pix * a.ldg + n);
+          if (r1g) o1[k] = *(const u32x2*)(r1g + pix * a.ldr1 + n);
         }
-    };
-    c16_epilogue<T, TN, TN, 0>(a, ct, rowpix, n0 + wc * 96, sbias + wc * 96, lane, stage);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const floatx4 bv = *(const floatx4*)(sbias + wc * 96 + j * 32 + 8 * k + 4 * lh);
+          float w[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = acc[j][4 * k + e] + bv[e];
+          if (gg) {   // GDN / IGDN: g / sqrt(n), g * rsqrt(n), g * sqrt(n)
+            const T* ge = (const T*)&og[k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float g = to_f(ge[e]);
+              w[e] = epi == LIC_EPI_GDN_DIV ? g / sqrtf(w[e]) : (epi == LIC_EPI_GDN_RSQRT ? g * (1.0f / sqrtf(w[e])) : g * sqrtf(w[e]));
+            }
+          } else if (act == LIC_ACT_GELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = gelu_f(w[e]);
+          } else if (act == LIC_ACT_LRELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : w[e] * a.slope;
+          } else if (act == LIC_ACT_RELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : 0.f;
+          }
+          if (r1g) {
+            const T* re = (const T*)&o1[k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] += to_f(re[e]);
+          }
+          u32x2 raw;
+          T* o = (T*)&raw;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = from_f<T>(w[e]);
+          *(u32x2*)(stg + l32 * 208 + (j * 32 + 8 * k + 4 * lh) * 2) = raw;
+        }
+      }
+      // destination of the tile's pixels, then the rows out as 16-B chunks (12 per pixel)
+      if (lh == 0) ((int64_t*)(stg + 32 * 208))[l32] = pok ? pix : -1;
+      wave_lds_sync();
+      T* __restrict__ yg = (T*)a.y;
+      T* __restrict__ y2g = (T*)a.y2;
+#pragma unroll
+      for (int h = 0; h < 6; ++h) {
+        const int idx = lane + 64 * h, pr = idx / 12, c = idx - pr * 12;
+        const u32x4 val = *(const u32x4*)(stg + pr * 208 + c * 16);
+        const int64_t dp = ((const int64_t*)(stg + 32 * 208))[pr];
+        if (dp >= 0) {
+          *(u32x4*)(yg + dp * a.ldy + nw + c * 8) = val;
+          if (y2g) *(u32x4*)(y2g + dp * a.ldy2 + nw + c * 8) = val;
+        }
+      }
+      wave_lds_sync();
+    } else {
+      // destination pixels of the tile's 32 rows (wave-private; the previous tile's epilogue has
+      // finished reading them: LDS requests of a wave complete in order)
+      if (lh == 0) {
+        int base = -1;
+        if (m < p.M) {
+          const int b = m / mij, rem = m - b * mij;
+          const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
+          int oy = a.oy0 + a.osy * i, ox = a.ox0 + a.osx * j;
+          if (a.out_shuffle >= 2) { oy *= 2; ox *= 2; }
+          base = (b * a.ho + oy) * a.wo + ox;
+        }
+        rowpix[l32] = base;
+      }
+      wave_lds_sync();
+      // epilogue (lic_common.h): stage each 32x32 tile as [pixel][channel] in the wave's slot, finish
+      // it with 16-B stores of consecutive channels, tile by tile
+      auto stage = [&](int q) {
+#pragma unroll
+        for (int qq = 0; qq < TN; ++qq)
+          if (qq == q) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ct[l32 * 33 + 8 * (r >> 2) + 4 * lh + (r & 3)] = acc[qq][r];
+          }
+      };
+      c16_epilogue<T, TN, TN, 0>(a, ct, rowpix, n0 + wc * 96, sbias + wc * 96, lane, stage);
+    }
     t = tn;
   }
 }
 
-template <typename T, int BN, int KST, int PRO>
+template <typename T, int BN, int KST, int PRO, int KT>
 void launch_g16(const lic_conv_args& a, const G16Plan& p, dim3 grid, int smem, hipStream_t s, int& status) {
-  const hipError_t ea = ensure_dyn_lds((const void*)gemm16_kernel<T, BN, KST, PRO>, smem);
+  auto kern = p.fast_epi ? gemm16_kernel<T, BN, KST, PRO, KT, true> : gemm16_kernel<T, BN, KST, PRO, KT, false>;
+  const hipError_t ea = ensure_dyn_lds((const void*)kern, smem);
   if (ea != hipSuccess) {
     status = fail(std::string("gemm16: dynamic LDS attribute: ") + hipGetErrorString(ea));
     return;
   }
-  hipLaunchKernelGGL((gemm16_kernel<T, BN, KST, PRO>), grid, dim3(512), smem, s, a, p);
+  hipLaunchKernelGGL(kern, grid, dim3(512), smem, s, a, p);
   hipError_t e = hipGetLastError();
   status = e == hipSuccess ? 0 : fail(std::string("gemm16 launch: ") + hipGetErrorString(e));
 }
 
+// The register epilogue: PLAIN (any of none / relu / lrelu / gelu) or GDN_DIV / _RSQRT / _SQRT, optional
+// r1, no r2; 16-B aligned outputs, 8-B aligned operands, whole 96-channel blocks, no pixel shuffle.
+inline bool g16_fast_epi_ok(const lic_conv_args& a) {
+  const bool gdn = a.epi == LIC_EPI_GDN_DIV || a.epi == LIC_EPI_GDN_RSQRT || a.epi == LIC_EPI_GDN_SQRT;
+  auto al16 = [](const void* ptr, int ld) { return ptr == nullptr || (((uintptr_t)ptr & 15) == 0 && ld % 8 == 0); };
+  auto al8 = [](const void* ptr, int ld) { return ptr == nullptr || (((uintptr_t)ptr & 7) == 0 && ld % 4 == 0); };
+  return (a.epi == LIC_EPI_PLAIN || gdn) && (gdn == (a.g != nullptr)) && a.out_shuffle == 0 && a.co == a.copad &&
+         a.act != LIC_ACT_ROUND && !(gdn && a.act != LIC_ACT_NONE) && al16(a.y, a.ldy) && al16(a.y2, a.ldy2) &&
+         al8(a.r1, a.ldr1) && al8(a.g, a.ldg);
+}
+
 // Returns 1 and launches when the gemm16 kernel applies; 0 to let the caller fall back.
-template <typename T, int BN, int KST>
+template <typename T, int BN, int KST, int KT = 1>
 int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
-  if (a.ntaps != 1 || a.copad % BN || a.out_shuffle != 0 || a.groups != 1) return 0;
+  if (a.ntaps != KT || a.copad % BN || a.out_shuffle != 0 || a.groups != 1) return 0;
   if ((a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE) || !c16_epi_supported(a)) return 0;
-  if (a.cpad != KST * 16 || a.ci != a.cpad || a.ldx % 8 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt % 16)) return 0;
+  if (a.ldx % 8 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt % 16)) return 0;
+  if (KT == 1 && KST > 1 && (a.cpad != KST * 16 || a.ci != a.cpad)) return 0;
+  // one 16-channel chunk per tap: Cin 8 (channels 8..15 read as zeros) or 16 (a 16-channel view)
+  if ((KT > 1 || KST == 1) && !(a.ci == 8 || (a.ci == 16 && a.ldx >= 16)) ) return 0;
+  if (KT > 1 && (KST != KT || a.prologue != LIC_PRO_NONE)) return 0;
   const int64_t xbytes = ((int64_t)a.n * a.h * a.w - 1) * a.ldx * 2 + (int64_t)a.ci * 2;
   const int64_t M = (int64_t)a.n * a.mi * a.mj;
   if (xbytes >= (1LL << 31) || M >= (1LL << 31) || (int64_t)a.n * a.ho * a.wo >= (1LL << 31)) return 0;
@@ -184,21 +307,31 @@ int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
   if (wgs > need) wgs = need;
   p.wgs = wgs;
   p.xrec = (unsigned)xbytes;
-  p.wrec = (unsigned)((int64_t)a.copad * a.cpad * 2);
-  const int smem = KST * BN * 32 + BN * 4 + 8 * 32 * 33 * 4 + 8 * 32 * 4;
+  p.wrec = (unsigned)((int64_t)a.copad * a.ntaps * a.cpad * 2);
+  const int smem = KST * BN * 32 + BN * 4 + 8 * G16_SLOT + 8 * 32 * 4;
+  p.fast_epi = g16_fast_epi_ok(a) && wd_env("LIC_G16_FAST_EPI", 1) ? 1 : 0;
   dim3 grid((unsigned)(wgs * p.nblk));
-  if (a.prologue == LIC_PRO_SQUARE) launch_g16<T, BN, KST, LIC_PRO_SQUARE>(a, p, grid, smem, s, status);
-  else launch_g16<T, BN, KST, LIC_PRO_NONE>(a, p, grid, smem, s, status);
+  if constexpr (KT > 1) launch_g16<T, BN, KST, LIC_PRO_NONE, KT>(a, p, grid, smem, s, status);
+  else if (a.prologue == LIC_PRO_SQUARE) launch_g16<T, BN, KST, LIC_PRO_SQUARE, 1>(a, p, grid, smem, s, status);
+  else launch_g16<T, BN, KST, LIC_PRO_NONE, 1>(a, p, grid, smem, s, status);
   return 1;
 }
 
-// Tile choice of the gemm16 kernel: 16-bit 1x1 convolutions with K in {96, 192} on maps of
-// >= 16 K output pixels.  LIC_GEMM16=0 restores the previous kernels (A/B).
+// Tile choice of the gemm16 kernel: 16-bit 1x1 convolutions with K in {96, 192} (or Cin 8 / 16) on
+// maps of >= 4 K output pixels, and 3x3 convolutions of Cin 8 / 16 (the image's first layer).
+// LIC_GEMM16=0 restores the previous kernels (A/B).
 template <typename T>
 int gemm16_dispatch_impl(const lic_conv_args& a, hipStream_t s, int& status) {
   static const int on = wd_env("LIC_GEMM16", 1);
-  if (!on || a.force_mfma_generic || a.force_direct || a.ntaps != 1) return 0;
-  if ((int64_t)a.n * a.mi * a.mj < 16384) return 0;
+  if (!on || a.force_mfma_generic || a.force_direct) return 0;
+  if ((int64_t)a.n * a.mi * a.mj < 4096) return 0;
+  if (a.ci <= 16) {   // the image's k x k layers and their 1x1 skips (one chunk per tap)
+    if (a.copad % 192 != 0) return 0;
+    if (a.ntaps == 9) return try_gemm16<T, 192, 9, 9>(a, s, status);
+    if (a.ntaps == 1) return try_gemm16<T, 192, 1, 1>(a, s, status);
+    return 0;
+  }
+  if (a.ntaps != 1) return 0;
   if (a.cpad == 192) {
     if (a.copad % 192 == 0) return try_gemm16<T, 192, 12>(a, s, status);
     if (a.copad % 96 == 0) return try_gemm16<T, 96, 12>(a, s, status);

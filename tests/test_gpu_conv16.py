@@ -196,3 +196,36 @@ def test_gemm16_gdn(dtype, variant):
     err = (out - ref).abs().max().item()
     scale = ref.abs().max().item()
     assert err <= (1e-2 if dtype == torch.float16 else 3e-2) * scale, (variant, err, scale)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("k,s,act", [(3, 2, "lrelu"), (1, 2, None), (3, 1, None)])
+def test_gemm16_image_layers(dtype, k, s, act):
+    """The image's first layers (ResidualBlockWithStride(3, 192): conv3x3 s2 + LeakyReLU and the 1x1
+    s2 skip, net_ga.py:271) on the 3-channel image zero-padded to 8 channels (Act.zpad): gemm16's
+    tap mode, one 16-channel K step per tap with channels 8..15 read as zeros."""
+    from lic_amd.layers import Conv2d
+    from lic_amd.functional import Act
+    from lic_amd import _ffi as L
+    torch.manual_seed(73 + k * 10 + s)
+    m = Conv2d(3, 192, k, s, k // 2)
+    x = torch.rand(8, 3, 128, 128) * 2 - 1
+    kw = dict(act=L.ACT_LRELU) if act else {}
+    out = m.to(DEV).run(Act.from_nchw(x.to(DEV), dtype, pad16=True), **kw).nchw()
+    ref = F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), s, k // 2)
+    if act:
+        ref = F.leaky_relu(ref)
+    _check(out, ref, dtype, f"image layer k{k} s{s} {dtype}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_gemm16_small_map_linear(dtype):
+    """1x1 layers on the 16x16 latents (B=32: 8192 pixels, the Swin / WBA Linears of the slice loop)."""
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(74)
+    for ci, co in ((192, 576), (192, 192)):
+        m = Conv2d(ci, co, 1, 1, 0)
+        x = torch.randn(32, ci, 16, 16) * 0.5
+        out = m.to(DEV).run(_act(x, dtype)).nchw()
+        ref = F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu())
+        _check(out, ref, dtype, f"1x1 {ci}->{co} @16x16 {dtype}")

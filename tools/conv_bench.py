@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--auto-only", action="store_true")
+    ap.add_argument("--gdn", default="", choices=["", "gdn", "gdn_r1", "igdn"],
+                    help="1x1 shapes through Fn.gdn (x^2 prologue, GDN epilogue; gdn_r1: + residual)")
     args = ap.parse_args()
     import lic_amd.functional as Fn
     from lic_amd.layers import Conv2d
@@ -70,22 +72,35 @@ def main():
         m = Conv2d(ci, co, k, s, 0).to(dev)
         x = Fn.Act(torch.randn(args.batch, H, H, ci, device=dev).to(dt))
         pk = m.packed(dt, pad)
+        if args.gdn:
+            if k != 1 or ci != co:
+                continue
+            from lic_amd.layers.gdn import GDN
+            g = GDN(ci, inverse=args.gdn == "igdn").to(dev)
+            pk = g.packed(dt)
+            r1 = Fn.Act(torch.randn(args.batch, H, H, ci, device=dev).to(dt)) if args.gdn == "gdn_r1" else None
+            from lic_amd._ffi import EPI_GDN_RSQRT, EPI_GDN_SQRT
+            mode = EPI_GDN_SQRT if args.gdn == "igdn" else EPI_GDN_RSQRT
+            Fn_conv = lambda x_, pk_, out_, **kw_: Fn.gdn(x_, pk_, mode, out_, r1)
         Ho, Wo = Fn.conv_out_hw(H, H, pk)
         out = Fn.Act.empty(args.batch, Ho, Wo, co, dt, dev)
         flops = 2.0 * args.batch * Ho * Wo * co * ci * k * k
+        conv_fn = Fn_conv if args.gdn else Fn.conv
         res = {}
         for variant in (("auto",) * 3 if args.auto_only else ("auto", "generic", "auto", "generic")):
             kw = dict(force_generic=(variant == "generic"))
             for _ in range(2):
-                Fn.conv(x, pk, out, **kw)
+                conv_fn(x, pk, out, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for _ in range(args.iters):
-                Fn.conv(x, pk, out, **kw)
+                conv_fn(x, pk, out, **kw)
             e1.record(st)
             e1.synchronize()
             t = e0.elapsed_time(e1) / 1e3 / args.iters
             res.setdefault(variant, []).append(t)
+        if args.gdn:
+            name = f"{args.gdn}:{name}"
         line = f"{name:18s} {flops / 1e9:8.1f} GFLOP"
         for v, ts in res.items():
             t = min(ts)
