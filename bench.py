@@ -365,7 +365,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--post-processing", action="store_true", help="HAN post-processing head (eval_net flag)")
     ap.add_argument("--profile", action="store_true",
-                    help="only warm-up + timed replays (for rocprofv3 per-forward kernel breakdowns)")
+                    help="only warm-up + timed replays (for rocprofv3 per-forward kernel breakdowns); the replays "
+                         "start after a 1-s idle gap (profiles/summarize.py --after-gap keeps them alone)")
+    ap.add_argument("--profile-a-model", action="store_true",
+                    help="with --profile: replay the a_model (g_a) graph instead of the whole forward")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group check without a GPU: gloo backend, no CUDA call; each rank "
                          "'processes' its batch as a no-op and rank 0 prints the JSON line's launch fields")
@@ -409,6 +412,14 @@ def main():
     def step():
         return net(x, "test")
 
+    if args.profile and args.profile_a_model:
+        from lic_amd.functional import Act, split_f32
+        xin = Act(x.to(dtype).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1))
+
+        def step():
+            with split_f32(SPLIT_MODES.get(net.precision, 0)):
+                return net.a_model.run(xin)
+
     for _ in range(max(1, args.warmup)):
         step()
     if args.no_graph:
@@ -417,6 +428,8 @@ def main():
         graph, _ = capture(step)
         run = graph.replay
     torch.cuda.synchronize()
+    if args.profile:
+        time.sleep(1.0)   # an idle gap between the warm-up / capture dispatches and the replays
 
     def timed(k):
         D.barrier(world)

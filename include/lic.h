@@ -547,15 +547,34 @@ typedef struct lic_wba_args {
 } lic_wba_args;
 int lic_wba_qkv_attn_fwd(const lic_wba_args* a, lic_stream_t stream);
 
+/* 16-bit (fp16 / bf16) WinBasedAttention core in one launch (csrc/wba16.hip; ABI 7): the qkv Linear
+ * (the 16-bit packed [3C][1][C] weights of its ConvPack, fp32 bias) + shifted-window attention with
+ * the unfused launches' arithmetic (q, k, v rounded to the 16-bit type after the bias, the scale on
+ * the fp32 dot); out = the C-channel attention output the proj Linear consumes.  C = 192, 8 heads,
+ * 8x8 windows, H and W multiples of 8; x 16-B aligned rows of 8k elements, out 8-B aligned.
+ * Replaces model/layers.py WinBasedAttention's qkv + attention (reference layers/win_attention.py:85-116). */
+typedef struct lic_wba16_args {
+  int32_t dtype;                             /* LIC_F16 or LIC_BF16 */
+  const void* x; int32_t n, h, w, c, ldx;    /* NHWC input (the block's x), c = 192 */
+  void* out; int32_t ldo;                    /* NHWC attention output, c channels */
+  int32_t heads, ws, shift, mask_kind;       /* 8, 8, shift, 1 */
+  float scale;                               /* head_dim ** -0.5 */
+  const float* table; int32_t tab_sr, tab_sh;
+  const void* qkv_w;                         /* [3C][1][C] packed weights, same dtype as x */
+  const float* qkv_bias;                     /* [3C] */
+} lic_wba16_args;
+int lic_wba16_qkv_attn_fwd(const lic_wba16_args* a, lic_stream_t stream);
+
 /* Library info.
  * LIC_ABI_VERSION changes whenever an entry point's parameter list or an args struct's layout
  * changes (3: lic_conv_args.mfma_mode / wgt_split, lic_rate_train_* seed_dev / seed_mul; 5:
- * lic_resunit_args / lic_resunit_fwd; 6: lic_wba_args / lic_wba_qkv_attn_fwd).  A
+ * lic_resunit_args / lic_resunit_fwd; 6: lic_wba_args / lic_wba_qkv_attn_fwd; 7: lic_wba16_args /
+ * lic_wba16_qkv_attn_fwd).  A
  * caller compiled against this header checks lic_abi_version() == LIC_ABI_VERSION and
  * lic_args_size(k) == sizeof(...) once after loading the library (the Python host does, _ffi.load). */
-#define LIC_ABI_VERSION 6
+#define LIC_ABI_VERSION 7
 enum { LIC_ARGS_CONV = 0, LIC_ARGS_ATTN = 1, LIC_ARGS_RATE = 2, LIC_ARGS_RANS = 3, LIC_ARGS_WGRAD = 4,
-       LIC_ARGS_RESUNIT = 5, LIC_ARGS_WBA = 6 };
+       LIC_ARGS_RESUNIT = 5, LIC_ARGS_WBA = 6, LIC_ARGS_WBA16 = 7 };
 const char* lic_last_error(void);
 const char* lic_version(void);          /* "liblic <ver> gfx950 (abi N, src <source hash>)" */
 /* Build provenance: the first 16 hex digits of the SHA-256 of the sources the library was built

@@ -33,7 +33,7 @@ ACT_NONE, ACT_RELU, ACT_LRELU, ACT_GELU, ACT_ROUND = 0, 1, 2, 3, 4
 PRO_NONE, PRO_SQUARE, PRO_ABS = 0, 1, 2
 EPI_PLAIN, EPI_GATE, EPI_HALF_TANH, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, EPI_RES_ACT = 0, 1, 2, 3, 4, 5, 6
 MAX_TAPS = 64
-ABI_VERSION = 6   # include/lic.h LIC_ABI_VERSION
+ABI_VERSION = 7   # include/lic.h LIC_ABI_VERSION
 
 EXPORTED_SYMBOLS = (
     "lic_conv2d_fwd", "lic_gdn_prepare", "lic_win_attn_fwd", "lic_layernorm_fwd",
@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "lic_layernorm_bwd", "lic_gate_fwd", "lic_half_tanh_fwd", "lic_half_tanh_bwd", "lic_avgpool_bwd",
     "lic_rate_train_parts", "lic_rate_train_fwd", "lic_rate_train_bwd", "lic_recon_train_blocks",
     "lic_recon_train_fwd", "lic_recon_train_bwd", "lic_dwconv_wgrad_workspace", "lic_dwconv_wgrad",
-    "lic_resunit_fwd", "lic_patches", "lic_wba_qkv_attn_fwd", "lic_pack_taps",
+    "lic_resunit_fwd", "lic_patches", "lic_wba_qkv_attn_fwd", "lic_wba16_qkv_attn_fwd", "lic_pack_taps",
     "lic_pack_taps_batch", "lic_pack_block_elems",
 )
 LIC_EB_PARAMS = 58
@@ -159,6 +159,19 @@ class WbaArgs(ctypes.Structure):
     ]
 
 
+class Wba16Args(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i32),
+        ("x", _vp), ("n", _i32), ("h", _i32), ("w", _i32), ("c", _i32), ("ldx", _i32),
+        ("out", _vp), ("ldo", _i32),
+        ("heads", _i32), ("ws", _i32), ("shift", _i32), ("mask_kind", _i32),
+        ("scale", _f32),
+        ("table", _vp), ("tab_sr", _i32), ("tab_sh", _i32),
+        ("qkv_w", _vp),
+        ("qkv_bias", _vp),
+    ]
+
+
 class RansArgs(ctypes.Structure):
     _fields_ = [
         ("n", _i32), ("hw", _i32), ("c", _i32), ("ctot", _i32), ("c0", _i32),
@@ -252,6 +265,7 @@ def load():
         "lic_dwconv_wgrad": [I, V, I, V, I, I, I, I, I, I, I, I, I, V, V, V, V, L, V],
         "lic_resunit_fwd": [V, V],
         "lic_wba_qkv_attn_fwd": [V, V],
+        "lic_wba16_qkv_attn_fwd": [V, V],
         "lic_patches": [I, V, I, I, I, I, I, I, I, I, I, V, V, V, I, I, V],
     }
     for name, argt in sig.items():
@@ -288,7 +302,7 @@ def load():
     if abi != ABI_VERSION:
         _load_error = f"liblic ABI {abi} at {path}, this host expects {ABI_VERSION}: rebuild liblic.so"
         raise LicError(_load_error)
-    for which, st in enumerate((ConvArgs, AttnArgs, RateArgs, RansArgs, WgradArgs, ResunitArgs, WbaArgs)):
+    for which, st in enumerate((ConvArgs, AttnArgs, RateArgs, RansArgs, WgradArgs, ResunitArgs, WbaArgs, Wba16Args)):
         if lib.lic_args_size(which) != ctypes.sizeof(st):
             _load_error = (f"liblic args struct {st.__name__}: library {lib.lic_args_size(which)} bytes, "
                            f"host {ctypes.sizeof(st)}: rebuild liblic.so")

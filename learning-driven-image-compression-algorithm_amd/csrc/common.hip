@@ -47,6 +47,7 @@ extern "C" int64_t lic_args_size(int32_t which) {
     case LIC_ARGS_WGRAD: return (int64_t)sizeof(lic_wgrad_args);
     case LIC_ARGS_RESUNIT: return (int64_t)sizeof(lic_resunit_args);
     case LIC_ARGS_WBA: return (int64_t)sizeof(lic_wba_args);
+    case LIC_ARGS_WBA16: return (int64_t)sizeof(lic_wba16_args);
     default: return -1;
   }
 }

@@ -65,8 +65,9 @@ __device__ __forceinline__ void c16_static_for(F&& f) {
 }
 
 // The epilogue variants the conv16 / gemm16 launches take (lic_common.h epilogue_run on NQ staged
-// 32 x 32 tiles, ct + q * 32 * 33): plain, + r1, gate (g, r1, r2), GDN (g), and the scalar path
-// (unaligned views, pixel shuffle).  Fewer compiled variants than epilogue_all's seven.
+// 32 x 32 tiles, ct + q * 32 * 33): plain, + r1, gate (g, r1, r2), GDN (g; + r1: ResidualBlockWithStride's
+// GDN + skip), and the scalar path (unaligned views, pixel shuffle).  Fewer compiled variants than
+// epilogue_all's seven.
 inline int c16_epi_mask_host(const lic_conv_args& a) {
   const bool gdn = a.epi == LIC_EPI_GDN_DIV || a.epi == LIC_EPI_GDN_RSQRT || a.epi == LIC_EPI_GDN_SQRT;
   return ((gdn || a.epi == LIC_EPI_GATE) ? EPI_G : 0) | ((a.r1 != nullptr && a.epi != LIC_EPI_HALF_TANH) ? EPI_R1 : 0) |
@@ -74,23 +75,33 @@ inline int c16_epi_mask_host(const lic_conv_args& a) {
 }
 inline bool c16_epi_supported(const lic_conv_args& a) {
   const int m = c16_epi_mask_host(a);
-  return m == 0 || m == EPI_R1 || m == EPI_G || m == (EPI_G | EPI_R1 | EPI_R2);
+  return m == 0 || m == EPI_R1 || m == EPI_G || m == (EPI_G | EPI_R1) || m == (EPI_G | EPI_R1 | EPI_R2);
 }
-template <typename T, int NQ, int TN, int CT_STRIDE, typename Stage>
+// VMASKS: the operand sets that get a vector variant (bit 0: none, 1: r1, 2: g, 3: g + r1, 4: g + r1 + r2);
+// any other set, and unaligned views, take the scalar path (each variant is a copy of the epilogue
+// loop: conv16's 12-tile kernels spill with more than two of them)
+template <typename T, int NQ, int TN, int CT_STRIDE, int VMASKS, typename Stage>
 __device__ __forceinline__ void c16_epilogue(const lic_conv_args& a, float* ct, const int* rowpix, int n0,
                                              const float* sbias, int lane, Stage& stage) {
-  if (!epi_vec_ok<T>(a)) {
-    epilogue_run<T, NQ, TN, -1, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
-    return;
+  const int m = epi_vec_ok<T>(a) ? epi_mask(a) : -1;
+  if constexpr ((VMASKS & 1) != 0) {
+    if (m == 0) return epilogue_run<T, NQ, TN, 0, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
   }
-  switch (epi_mask(a)) {
-    case 0: epilogue_run<T, NQ, TN, 0, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage); break;
-    case EPI_R1: epilogue_run<T, NQ, TN, EPI_R1, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage); break;
-    case EPI_G: epilogue_run<T, NQ, TN, EPI_G, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage); break;
-    default:
-      epilogue_run<T, NQ, TN, EPI_G | EPI_R1 | EPI_R2, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
-      break;
+  if constexpr ((VMASKS & 2) != 0) {
+    if (m == EPI_R1) return epilogue_run<T, NQ, TN, EPI_R1, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
   }
+  if constexpr ((VMASKS & 4) != 0) {
+    if (m == EPI_G) return epilogue_run<T, NQ, TN, EPI_G, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
+  }
+  if constexpr ((VMASKS & 8) != 0) {
+    if (m == (EPI_G | EPI_R1))
+      return epilogue_run<T, NQ, TN, EPI_G | EPI_R1, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
+  }
+  if constexpr ((VMASKS & 16) != 0) {
+    if (m == (EPI_G | EPI_R1 | EPI_R2))
+      return epilogue_run<T, NQ, TN, EPI_G | EPI_R1 | EPI_R2, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
+  }
+  epilogue_run<T, NQ, TN, -1, Stage, CT_STRIDE>(a, ct, rowpix, n0, sbias, lane, stage);
 }
 
 // One LDS-DMA piece: 64 lanes x 16 B from rsrc + voffset + soffset to lds + 16 * lane.  (In a
@@ -107,7 +118,7 @@ struct C16Plan {
   unsigned xrec;      // bytes addressable from a.x (buffer range; past it loads read zeros)
   unsigned wrec;      // bytes of the packed weights
   int nst;            // stages = nchunks * ngroups
-  int fast_epi;       // 1: the register epilogue applies (c16_fast_epi_ok)
+  int fast_epi;       // the register epilogue variant (c16_fast_epi): 0 none, 1 plain / + r1, 2 gate
 };
 
 // S = 1: stages are (chunk, group of G taps = G/KW tap rows).  S = 2: stages are (chunk, input-parity
@@ -141,7 +152,9 @@ struct C16Geo {
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
-template <typename T, int KH, int KW, int S, int G, int BN, int WN, bool FAST>
+// FAST: 0 = the shared epilogue (c16_epilogue), 1 = the register epilogue (plain / + r1), 2 = the
+// register epilogue of the Win_noShift_Attention gate g * sigmoid(act(acc + b) + r1) + r2
+template <typename T, int KH, int KW, int S, int G, int BN, int WN, int FAST>
 __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, const C16Plan p) {
   using Geo = C16Geo<KH, KW, S, G, BN, WN>;
   constexpr int NW = Geo::NW, PJ = Geo::PJ, CT = Geo::CT, HWD = Geo::HWD;
@@ -370,20 +383,32 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
     T* __restrict__ yg = (T*)a.y;
     T* __restrict__ y2g = (T*)a.y2;
     const T* __restrict__ r1g = (const T*)a.r1;
+    const T* __restrict__ gg = (const T*)a.g;
+    const T* __restrict__ r2g = (const T*)a.r2;
     const int act = a.act;
     const float slope = a.slope;
     c16_static_for<0, CT * PJ>([&](auto qc) {
       constexpr int q = decltype(qc)::value, i = q % CT, j = q / CT;
       const int row = i0 + wr * PJ + j;
       const int nloc = wc * Geo::WCH + i * 32;       // channel of the tile's first column, in the block
-      // residual operand, in the accumulator layout (8 B = 4 channels per lane and run)
-      u32x2 rr[4];
-      if (r1g) {
+      // residual / gate operands, in the accumulator layout (8 B = 4 channels per lane and run)
+      u32x2 rr[4], rg[4], r2v[4];
+      if (FAST == 2 || r1g) {
         const int col = j0 + l32;
         const bool ok = row < a.mi && col < a.mj;
         const int64_t pix = ok ? ((int64_t)b * a.ho + a.oy0 + a.osy * row) * a.wo + a.ox0 + a.osx * col : 0;
+        const int nb = n0 + nloc + 4 * lh;
+        if (r1g) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) rr[k] = *(const u32x2*)(r1g + pix * a.ldr1 + n0 + nloc + 8 * k + 4 * lh);
+          for (int k = 0; k < 4; ++k) rr[k] = *(const u32x2*)(r1g + pix * a.ldr1 + nb + 8 * k);
+        }
+        if constexpr (FAST == 2) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            rg[k] = *(const u32x2*)(gg + pix * a.ldg + nb + 8 * k);
+            r2v[k] = *(const u32x2*)(r2g + pix * a.ldr2 + nb + 8 * k);
+          }
+        }
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -397,11 +422,20 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
         } else if (act == LIC_ACT_RELU) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : 0.f;
+        } else if (BN == 96 && act == LIC_ACT_GELU) {   // (ResidualBottleneck's 3x3; 4 tiles a wave)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = gelu_f(w[e]);
         }
         if (r1g) {
           const T* re = (const T*)&rr[k];
 #pragma unroll
           for (int e = 0; e < 4; ++e) w[e] += to_f(re[e]);
+        }
+        if constexpr (FAST == 2) {   // gate: g * sigmoid(.) + r2
+          const T* ge = (const T*)&rg[k];
+          const T* r2e = (const T*)&r2v[k];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = to_f(ge[e]) * sigmoid_f(w[e]) + to_f(r2e[e]);
         }
         u32x2 raw;
         T* o = (T*)&raw;
@@ -425,8 +459,9 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
       wave_lds_sync();
     });
   } else {
-    c16_epilogue<T, CT * PJ, CT, 0>(a, ct, rowpix + wr * PJ * 32, n0 + wc * Geo::WCH, sbias + wc * Geo::WCH, lane,
-                                    stage_tile);
+    // (plain and + r1 only: the gate has its register variant, the rest is rare -- scalar)
+    c16_epilogue<T, CT * PJ, CT, 0, 3>(a, ct, rowpix + wr * PJ * 32, n0 + wc * Geo::WCH, sbias + wc * Geo::WCH, lane,
+                                       stage_tile);
   }
 #if C16_STAMP
   C16T(t_end);
@@ -443,14 +478,20 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
 #endif
 }
 
-// The register epilogue: plain or + r1 (PLAIN), activation none / relu / lrelu (GELU's erf would bloat it),
-// every view 16-B aligned with rows of whole 16-B chunks, whole 32-channel tiles, no pixel shuffle.
-inline bool c16_fast_epi_ok(const lic_conv_args& a, int esz) {
+// The register epilogue: 1 = plain or + r1 (PLAIN), 2 = the gate (GATE with g, r1, r2); activation none /
+// relu / lrelu, and GELU on the 96-channel blocks (its erf would bloat the 12-tile variants), outputs 16-B aligned with rows of whole 16-B chunks, operands
+// 8-B aligned, whole 32-channel tiles, no pixel shuffle.  0: the shared epilogue.
+inline int c16_fast_epi(const lic_conv_args& a, int esz, bool gelu_ok) {
   auto al = [&](const void* ptr, int ld) { return ptr == nullptr || (((uintptr_t)ptr & 15) == 0 && (ld * esz) % 16 == 0); };
+  auto al8 = [&](const void* ptr, int ld) { return ptr == nullptr || (((uintptr_t)ptr & 7) == 0 && (ld * esz) % 8 == 0); };
   const int m = c16_epi_mask_host(a);
-  return (m == 0 || m == EPI_R1) && a.epi == LIC_EPI_PLAIN && a.out_shuffle == 0 && a.co == a.copad &&
-         (a.act == LIC_ACT_NONE || a.act == LIC_ACT_RELU || a.act == LIC_ACT_LRELU) &&
-         al(a.y, a.ldy) && al(a.y2, a.ldy2) && (a.r1 == nullptr || (((uintptr_t)a.r1 & 7) == 0 && a.ldr1 % 4 == 0));
+  if (!(a.out_shuffle == 0 && a.co == a.copad &&
+        (a.act == LIC_ACT_NONE || a.act == LIC_ACT_RELU || a.act == LIC_ACT_LRELU || (gelu_ok && a.act == LIC_ACT_GELU)) &&
+        al(a.y, a.ldy) && al(a.y2, a.ldy2) && al8(a.r1, a.ldr1) && al8(a.g, a.ldg) && al8(a.r2, a.ldr2)))
+    return 0;
+  if ((m == 0 || m == EPI_R1) && a.epi == LIC_EPI_PLAIN) return 1;
+  if (m == (EPI_G | EPI_R1 | EPI_R2) && a.epi == LIC_EPI_GATE) return 2;
+  return 0;
 }
 
 // Returns 1 and launches when the conv16 kernel applies; 0 to let the caller fall back.
@@ -475,10 +516,11 @@ int try_conv16(const lic_conv_args& a, hipStream_t s, int& status) {
   p.xrec = (unsigned)xbytes;
   p.wrec = (unsigned)wbytes;
   p.nst = p.nchunks * Geo::NG;
-  p.fast_epi = c16_fast_epi_ok(a, 2) && wd_env("LIC_C16_FAST_EPI", 1) ? 1 : 0;
+  p.fast_epi = wd_env("LIC_C16_FAST_EPI", 1) ? c16_fast_epi(a, 2, BN == 96) : 0;
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   dim3 grid((unsigned)blocks, a.copad / BN);
-  auto kern = p.fast_epi ? conv16_kernel<T, KH, KW, S, G, BN, WN, true> : conv16_kernel<T, KH, KW, S, G, BN, WN, false>;
+  auto kern = p.fast_epi == 1 ? conv16_kernel<T, KH, KW, S, G, BN, WN, 1> : conv16_kernel<T, KH, KW, S, G, BN, WN, 0>;
+  if (p.fast_epi == 2) kern = conv16_kernel<T, KH, KW, S, G, BN, WN, 2>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, Geo::SMEM);
   if (ea != hipSuccess) {
     status = fail(std::string("conv16: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -490,22 +532,43 @@ int try_conv16(const lic_conv_args& a, hipStream_t s, int& status) {
   return 1;
 }
 
-// Tile choice of the conv16 kernel (16-bit, stride-1 3x3 / 7x7 and stride-2 5x5 on output maps with
-// >= 16 x 32 pixels and enough tiles to fill the chip).  LIC_CONV16=0 restores the halo kernel (A/B).
+}  // namespace lic
+
+#include "conv16s.h"
+
+namespace lic {
+
+// Tile choice of the conv16 kernels (16-bit): conv16 for stride-1 3x3 and stride-2 5x5 on output maps
+// with >= 16 x 32 pixels and enough tiles to fill the chip; conv16s for stride-1 3x3 / 7x7 on the
+// maps conv16 does not fill (the 16 x 16 latents).  LIC_CONV16=0 restores the halo kernel (A/B);
+// LIC_CONV16S=0 keeps small maps on it, =2 takes conv16s wherever it applies (A/B).
 template <typename T>
 int conv16_dispatch_impl(const lic_conv_args& a, hipStream_t s, int& status) {
   static const int on = wd_env("LIC_CONV16", 1);
+  static const int small_on = wd_env("LIC_CONV16S", 1);
   if (!on || a.force_mfma_generic || a.force_direct) return 0;
-  if (a.mi < 16 || a.mj < 32) return 0;
   auto blocks = [&](int bn) { return (int64_t)a.n * ((a.mi + 15) / 16) * ((a.mj + 31) / 32) * (a.copad / bn); };
+  const bool big = a.mi >= 16 && a.mj >= 32 && small_on != 2;
   if (a.isy == 1 && a.isx == 1) {
-    if (a.ntaps == 9) {
+    if (a.ntaps == 9 && big) {
       if (a.copad % 192 == 0 && blocks(192) >= 128) return try_conv16<T, 3, 3, 1, 9, 192, 2>(a, s, status);
       if (a.copad % 96 == 0 && blocks(96) >= 128) return try_conv16<T, 3, 3, 1, 9, 96, 1>(a, s, status);
     }
-    // (7x7 stays on the halo kernel: the 7 tap-column bases next to 12 accumulator tiles and the
-    // epilogue's operand sets spilled 536 VGPRs, 1.9 ms against 0.40)
+    // 7x7: one tap row per stage (7 stages per chunk).  With the unrolled epilogue of round 5's first
+    // version the 7 tap-column bases next to 12 accumulator tiles spilled 536 VGPRs (1.9 ms against the
+    // halo kernel's 0.40); with the compact epilogues 18.  A/B: LIC_CONV16_7X7=0 (halo kernel)
+    if (a.ntaps == 49 && big && a.copad % 192 == 0 && blocks(192) >= 128 && wd_env("LIC_CONV16_7X7", 1))
+      return try_conv16<T, 7, 7, 1, 7, 192, 2>(a, s, status);
+    const bool small_map = !(a.mi >= 16 && a.mj >= 32 && blocks(96) >= 128);
+    if (small_on && (small_map || small_on == 2) && (a.ntaps == 9 || (a.ntaps == 49 && small_map))) {
+      auto sblocks = [&](int ct) { return (int64_t)a.n * ((a.mi + 3) / 4) * ((a.mj + 15) / 16) * (a.copad / (32 * ct)); };
+      if (a.ntaps == 49) return a.copad % 96 == 0 && try_conv16s<T, 7, 7, 3>(a, s, status);
+      if (a.copad % 96 == 0 && sblocks(3) >= 128) return try_conv16s<T, 3, 3, 3>(a, s, status);
+      if (a.copad % 64 == 0 && sblocks(2) >= 128) return try_conv16s<T, 3, 3, 2>(a, s, status);
+      if (a.copad % 32 == 0) return try_conv16s<T, 3, 3, 1>(a, s, status);
+    }
   }
+  if (a.mi < 16 || a.mj < 32) return 0;
   // ZeroPad2d((1,2,1,2)) + conv5x5 s2 (the a_model's downsampling convs): four input-parity phases
   if (a.isy == 2 && a.isx == 2 && a.ntaps == 25 && a.copad % 192 == 0 && blocks(192) >= 128 &&
       wd_env("LIC_CONV16_S2", 1))

@@ -14,6 +14,7 @@
 //     32 x 32 tile in a wave-private LDS slot and stores 16 B of consecutive channels per lane.
 // MFMA is a quarter busy at the HBM rate: the bound is the bytes (x once, y once per N block).
 #pragma once
+#include <cstdio>
 #include "conv16.h"
 
 namespace lic {
@@ -29,14 +30,17 @@ struct G16Plan {
   int wgs;        // workgroups per channel block
   unsigned xrec;  // bytes addressable from a.x
   unsigned wrec;  // bytes of the packed weights
-  int fast_epi;   // 1: the register epilogue (g16_fast_epi_ok)
+  int fast_epi;   // 1: the register epilogue (g16_fast_epi_ok); 2: + GDN g from the fragments (g16_gx_ok)
 };
 
 // KT = 1: a 1x1 convolution, K step kk = input channels 16kk .. 16kk+15.  KT > 1: a small-Cin k x k
 // convolution (the image's first layers: Cin 8 or 16, any stride) as an implicit GEMM without a halo:
 // K step kk = tap kk's 16 channels, each lane loading its pixel's tap directly (the taps' re-reads of
 // neighbouring pixels are L1 / L2 hits); channels 8..15 read zeros when Cin is 8.
-template <typename T, int BN, int KST, int PRO, int KT = 1, bool FAST = false>
+// FAST: 0 = the shared epilogue (c16_epilogue), 1 = the register epilogue, 2 = the register epilogue of
+// a GDN whose g is the layer's own input at the output pixel (g16_gx_ok): g is taken from this tile's
+// B-fragment registers (the x^2 prologue squares a copy) instead of being loaded again.
+template <typename T, int BN, int KST, int PRO, int KT = 1, int FAST = 0>
 __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, const G16Plan p) {
   // a wave computes 32 pixels x 96 channels (3 accumulator tiles); at BN = 192 two waves share each
   // pixel tile (its fragments are loaded twice, from L2 the second time)
@@ -118,17 +122,30 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
   int t = __builtin_amdgcn_readfirstlane(rank * NSTREAM + wst);   // uniform: a scalar loop
   u32x4 xc[KST];
   if (t < p.ntiles) load_tile(t, xc);
-  while (t < p.ntiles) {
-    if constexpr (PRO == LIC_PRO_SQUARE) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  // x^2 of 8 16-bit values, rounded once (the exact product rounded to T): fp16 by packed-f16 multiplies
+  // (v_pk_mul_f16, 4 per fragment instead of 8 x convert / multiply / convert -- the VALU, not the
+  // MFMA, bounded the GDN launches)
+  auto square = [&](u32x4 v) __attribute__((always_inline)) -> u32x4 {
+    if constexpr (std::is_same<T, half_t>::value) {
+      typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+      h8 hv = __builtin_bit_cast(h8, v);
+      hv = hv * hv;
+      v = __builtin_bit_cast(u32x4, hv);
+    } else {
+      T* e = (T*)&v;
 #pragma unroll
-      for (int kk = 0; kk < KST; ++kk) {
-        T* e = (T*)&xc[kk];
-#pragma unroll
-        for (int z = 0; z < 8; ++z) {
-          const float f = to_f(e[z]);
-          e[z] = from_f<T>(f * f);
-        }
+      for (int z = 0; z < 8; ++z) {
+        const float f = to_f(e[z]);
+        e[z] = from_f<T>(f * f);
       }
+    }
+    return v;
+  };
+  while (t < p.ntiles) {
+    if constexpr (PRO == LIC_PRO_SQUARE && FAST != 2) {
+#pragma unroll
+      for (int kk = 0; kk < KST; ++kk) xc[kk] = square(xc[kk]);
     }
     floatx16 acc[TN];
 #pragma unroll
@@ -141,55 +158,94 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
     asm volatile("" : "+v"(wl));
 #pragma unroll
     for (int kk = 0; kk < KST; ++kk) {
+      u32x4 xv = xc[kk];
+      if constexpr (PRO == LIC_PRO_SQUARE && FAST == 2) xv = square(xv);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const u32x4 wf = *(const u32x4*)(smem + wl + (kk * BN + j * 32) * 32);
-        acc[j] = mfma_k16<T>(wf, xc[kk], acc[j]);
+        acc[j] = mfma_k16<T>(wf, xv, acc[j]);
       }
     }
     const int tn = __builtin_amdgcn_readfirstlane(t + stride);
-    if (tn < p.ntiles) load_tile(tn, xc);
     const int m = t * 32 + l32;
-    if constexpr (FAST) {
-      // Register epilogue: bias, activation, GDN (g = the layer's input at the pixel) and residual on
-      // the accumulators as they stand (lane = pixel, 4-channel runs), rounded, staged as 16-bit
-      // [pixel][96 channels] rows (208-B pitch) in the wave's slot, stored as 16 B of consecutive
-      // channels per lane (six 1-KB stores per tile).  ~40 instructions per 32 x 32 tile against
-      // ~250 for lic_common.h's epilogue_run.
-      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-      char* stg = (char*)ct;
-      const bool pok = m < p.M;
-      int64_t pix = 0;
+    // register epilogue: its operands are fetched BEFORE the next tile's loads are issued (loads retire
+    // in order: issued after them, waiting for an operand would wait for the whole next tile too)
+    u32x2 og[TN][4], o1[TN][4];
+    int64_t pix = 0;
+    const bool pok = m < p.M;
+    const int nw = n0 + wc * 96;
+    const T* __restrict__ gg = (const T*)a.g;
+    const T* __restrict__ r1g = (const T*)a.r1;
+    if constexpr (FAST != 0) {
       if (pok) {
         const int b = m / mij, rem = m - b * mij;
         const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
         pix = ((int64_t)b * a.ho + a.oy0 + a.osy * i) * a.wo + a.ox0 + a.osx * j;
       }
-      const int nw = n0 + wc * 96;
-      const T* __restrict__ gg = (const T*)a.g;
-      const T* __restrict__ r1g = (const T*)a.r1;
+      if constexpr (FAST == 2) {
+        // g at channel n = nw + 32j + 8k + 4lh + e: K step n / 16 = KB + 2j + k/2, fragment half k & 1,
+        // elements 4lh .. 4lh+3 of that half -- in this lane (half lh) or in its partner lane ^ 32
+        auto gx = [&](auto kbc) __attribute__((always_inline)) {
+          constexpr int KB = decltype(kbc)::value;
+          const int partner = (lane ^ 32) << 2;
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const u32x4 x = xc[KB + 2 * j + h2];
+              const unsigned own0 = lh ? x[2] : x[0], own1 = lh ? x[3] : x[1];
+              const unsigned rc0 = (unsigned)__builtin_amdgcn_ds_bpermute(partner, (int)(lh ? x[0] : x[2]));
+              const unsigned rc1 = (unsigned)__builtin_amdgcn_ds_bpermute(partner, (int)(lh ? x[1] : x[3]));
+              const u32x2 own = {own0, own1}, rcv = {rc0, rc1};
+              og[j][2 * h2] = lh ? rcv : own;       // half 0
+              og[j][2 * h2 + 1] = lh ? own : rcv;   // half 1
+            }
+        };
+        if constexpr (WS == 2) {
+          if (wc == 0) gx(std::integral_constant<int, 0>{});
+          else gx(std::integral_constant<int, 6>{});
+        } else {
+          gx(std::integral_constant<int, 0>{});
+        }
+      } else if (gg) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) og[j][k] = *(const u32x2*)(gg + pix * a.ldg + nw + j * 32 + 8 * k + 4 * lh);
+      }
+      if (r1g) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o1[j][k] = *(const u32x2*)(r1g + pix * a.ldr1 + nw + j * 32 + 8 * k + 4 * lh);
+      }
+    }
+    if (tn < p.ntiles) load_tile(tn, xc);
+    if constexpr (FAST != 0) {
+      // Register epilogue: bias, activation, GDN and residual on the accumulators as they stand (lane =
+      // pixel, 4-channel runs), rounded, staged as 16-bit [pixel][96 channels] rows (208-B pitch) in the
+      // wave's slot, stored as 16 B of consecutive channels per lane (six 1-KB stores per tile).
+      // ~40 instructions per 32 x 32 tile against ~250 for lic_common.h's epilogue_run.
+      char* stg = (char*)ct;
       const int epi = a.epi, act = a.act;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        u32x2 og[4], o1[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int n = nw + j * 32 + 8 * k + 4 * lh;
-          if (gg) og[k] = *(const u32x2*)(gg + pix * a.ldg + n);
-          if (r1g) o1[k] = *(const u32x2*)(r1g + pix * a.ldr1 + n);
-        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const floatx4 bv = *(const floatx4*)(sbias + wc * 96 + j * 32 + 8 * k + 4 * lh);
           float w[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) w[e] = acc[j][4 * k + e] + bv[e];
-          if (gg) {   // GDN / IGDN: g / sqrt(n), g * rsqrt(n), g * sqrt(n)
-            const T* ge = (const T*)&og[k];
+          if (FAST == 2 || gg) {
+            // GDN / IGDN: g / sqrt(n), g * rsqrt(n) -> g * rsq(n); g * sqrt(n) -> g * n * rsq(n).  v_rsq_f32
+            // (~1 ulp of fp32) instead of the IEEE sqrt + division sequences (~20 instructions an element):
+            // the result is rounded to the 16-bit type (2^-11 / 2^-8) right after
+            const T* ge = (const T*)&og[j][k];
+            const bool sq = epi == LIC_EPI_GDN_SQRT;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float g = to_f(ge[e]);
-              w[e] = epi == LIC_EPI_GDN_DIV ? g / sqrtf(w[e]) : (epi == LIC_EPI_GDN_RSQRT ? g * (1.0f / sqrtf(w[e])) : g * sqrtf(w[e]));
+              const float rs = __builtin_amdgcn_rsqf(w[e]);
+              w[e] = to_f(ge[e]) * (sq ? w[e] * rs : rs);
             }
           } else if (act == LIC_ACT_GELU) {
 #pragma unroll
@@ -202,7 +258,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
             for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : 0.f;
           }
           if (r1g) {
-            const T* re = (const T*)&o1[k];
+            const T* re = (const T*)&o1[j][k];
 #pragma unroll
             for (int e = 0; e < 4; ++e) w[e] += to_f(re[e]);
           }
@@ -254,7 +310,7 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
             for (int r = 0; r < 16; ++r) ct[l32 * 33 + 8 * (r >> 2) + 4 * lh + (r & 3)] = acc[qq][r];
           }
       };
-      c16_epilogue<T, TN, TN, 0>(a, ct, rowpix, n0 + wc * 96, sbias + wc * 96, lane, stage);
+      c16_epilogue<T, TN, TN, 0, 31>(a, ct, rowpix, n0 + wc * 96, sbias + wc * 96, lane, stage);
     }
     t = tn;
   }
@@ -262,7 +318,9 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
 
 template <typename T, int BN, int KST, int PRO, int KT>
 void launch_g16(const lic_conv_args& a, const G16Plan& p, dim3 grid, int smem, hipStream_t s, int& status) {
-  auto kern = p.fast_epi ? gemm16_kernel<T, BN, KST, PRO, KT, true> : gemm16_kernel<T, BN, KST, PRO, KT, false>;
+  auto kern = p.fast_epi == 1 ? gemm16_kernel<T, BN, KST, PRO, KT, 1> : gemm16_kernel<T, BN, KST, PRO, KT, 0>;
+  if constexpr (PRO == LIC_PRO_SQUARE && KT == 1 && BN == 192 && KST == 12)
+    if (p.fast_epi == 2) kern = gemm16_kernel<T, BN, KST, PRO, KT, 2>;
   const hipError_t ea = ensure_dyn_lds((const void*)kern, smem);
   if (ea != hipSuccess) {
     status = fail(std::string("gemm16: dynamic LDS attribute: ") + hipGetErrorString(ea));
@@ -284,19 +342,35 @@ inline bool g16_fast_epi_ok(const lic_conv_args& a) {
          al8(a.r1, a.ldr1) && al8(a.g, a.ldg);
 }
 
+// FAST 2: a GDN (x^2 prologue) whose g is the layer input itself at the output pixel and channel --
+// identity pixel map, Cin = Cout = 192 in one channel block -- so g is in the tile's fragments.
+inline bool g16_gx_ok(const lic_conv_args& a) {
+  return a.prologue == LIC_PRO_SQUARE && a.g == a.x && a.ldg == a.ldx && a.ci == 192 && a.cpad == 192 &&
+         a.co == 192 && a.copad == 192 && a.ntaps == 1 && a.dy[0] == 0 && a.dx[0] == 0 && a.isy == 1 &&
+         a.isx == 1 && a.oy0 == 0 && a.ox0 == 0 && a.osy == 1 && a.osx == 1 && a.ho == a.h && a.wo == a.w &&
+         a.mi == a.h && a.mj == a.w;
+}
+
 // Returns 1 and launches when the gemm16 kernel applies; 0 to let the caller fall back.
 template <typename T, int BN, int KST, int KT = 1>
 int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
-  if (a.ntaps != KT || a.copad % BN || a.out_shuffle != 0 || a.groups != 1) return 0;
-  if ((a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE) || !c16_epi_supported(a)) return 0;
-  if (a.ldx % 8 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt % 16)) return 0;
-  if (KT == 1 && KST > 1 && (a.cpad != KST * 16 || a.ci != a.cpad)) return 0;
+  // LIC_TRACE=1: name the condition that declines the launch (stderr)
+#define G16_DECLINE(cond)                                                                     \
+  if (cond) {                                                                                 \
+    if (wd_env("LIC_TRACE", 0)) fprintf(stderr, "gemm16<%d,%d,%d> declines: %s\n", BN, KST, KT, #cond); \
+    return 0;                                                                                 \
+  }
+  G16_DECLINE(a.ntaps != KT || a.copad % BN || a.out_shuffle != 0 || a.groups != 1)
+  G16_DECLINE((a.prologue != LIC_PRO_NONE && a.prologue != LIC_PRO_SQUARE) || !c16_epi_supported(a))
+  G16_DECLINE(a.ldx % 8 || ((uintptr_t)a.x % 16) || ((uintptr_t)a.wgt % 16))
+  G16_DECLINE(KT == 1 && KST > 1 && (a.cpad != KST * 16 || a.ci != a.cpad))
   // one 16-channel chunk per tap: Cin 8 (channels 8..15 read as zeros) or 16 (a 16-channel view)
-  if ((KT > 1 || KST == 1) && !(a.ci == 8 || (a.ci == 16 && a.ldx >= 16)) ) return 0;
-  if (KT > 1 && (KST != KT || a.prologue != LIC_PRO_NONE)) return 0;
+  G16_DECLINE((KT > 1 || KST == 1) && !(a.ci == 8 || (a.ci == 16 && a.ldx >= 16)))
+  G16_DECLINE(KT > 1 && (KST != KT || a.prologue != LIC_PRO_NONE))
   const int64_t xbytes = ((int64_t)a.n * a.h * a.w - 1) * a.ldx * 2 + (int64_t)a.ci * 2;
   const int64_t M = (int64_t)a.n * a.mi * a.mj;
-  if (xbytes >= (1LL << 31) || M >= (1LL << 31) || (int64_t)a.n * a.ho * a.wo >= (1LL << 31)) return 0;
+  G16_DECLINE(xbytes >= (1LL << 31) || M >= (1LL << 31) || (int64_t)a.n * a.ho * a.wo >= (1LL << 31))
+#undef G16_DECLINE
   G16Plan p;
   p.M = (int)M;
   p.ntiles = (int)((M + 31) / 32);
@@ -310,6 +384,7 @@ int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
   p.wrec = (unsigned)((int64_t)a.copad * a.ntaps * a.cpad * 2);
   const int smem = KST * BN * 32 + BN * 4 + 8 * G16_SLOT + 8 * 32 * 4;
   p.fast_epi = g16_fast_epi_ok(a) && wd_env("LIC_G16_FAST_EPI", 1) ? 1 : 0;
+  if (p.fast_epi && g16_gx_ok(a) && wd_env("LIC_G16_GX", 1)) p.fast_epi = 2;
   dim3 grid((unsigned)(wgs * p.nblk));
   if constexpr (KT > 1) launch_g16<T, BN, KST, LIC_PRO_NONE, KT>(a, p, grid, smem, s, status);
   else if (a.prologue == LIC_PRO_SQUARE) launch_g16<T, BN, KST, LIC_PRO_SQUARE, 1>(a, p, grid, smem, s, status);
@@ -323,6 +398,9 @@ int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
 template <typename T>
 int gemm16_dispatch_impl(const lic_conv_args& a, hipStream_t s, int& status) {
   static const int on = wd_env("LIC_GEMM16", 1);
+  if (wd_env("LIC_TRACE", 0))
+    fprintf(stderr, "gemm16 dispatch: n %d mi %d mj %d ci %d cpad %d co %d copad %d ntaps %d pro %d epi %d act %d\n", a.n,
+            a.mi, a.mj, a.ci, a.cpad, a.co, a.copad, a.ntaps, a.prologue, a.epi, a.act);
   if (!on || a.force_mfma_generic || a.force_direct) return 0;
   if ((int64_t)a.n * a.mi * a.mj < 4096) return 0;
   if (a.ci <= 16) {   // the image's k x k layers and their 1x1 skips (one chunk per tap)

@@ -774,6 +774,36 @@ def wba_qkv_attn(x: Act, qkv_pk: ConvPack, heads: int, ws: int, shift: int, tabl
     return out
 
 
+def wba16_qkv_attn_ok(x: Act, C: int, heads: int, ws: int) -> bool:
+    """The 16-bit fused qkv + window-attention launch applies (csrc/wba16.hip): fp16 / bf16, C = 192,
+    8 heads, 8x8 windows, H and W multiples of 8, 16-byte aligned rows of 8k elements."""
+    return (x.dtype in (torch.float16, torch.bfloat16) and C == 192 and heads == 8 and ws == 8 and x.c == C and
+            x.H % 8 == 0 and x.W % 8 == 0 and x.ld % 8 == 0 and x.ptr % 16 == 0)
+
+
+def wba16_qkv_attn(x: Act, qkv_pk: ConvPack, heads: int, ws: int, shift: int, table: torch.Tensor, tab_sr: int,
+                   tab_sh: int, mask_kind: int, scale: float, out: Optional[Act] = None) -> Act:
+    """lic_wba16_qkv_attn_fwd: qkv Linear + shifted-window attention of a 16-bit map in one launch
+    (the arithmetic of conv(x, qkv_pk) + win_attn(...): q, k, v rounded to the 16-bit type after the
+    bias); returns the C-channel attention output that the proj Linear consumes."""
+    C = x.c
+    if (qkv_pk.w.dtype != x.dtype or qkv_pk.copad != 3 * C or qkv_pk.cpad != C or qkv_pk.bias is None or
+            len(qkv_pk.dy) != 1 or qkv_pk.co != 3 * C):
+        raise _ffi.LicError("wba16_qkv_attn: the qkv pack must be a [3C][1][C] pack of the input's dtype with a bias")
+    if out is None:
+        out = Act.empty(x.B, x.H, x.W, C, x.dtype, x.t.device)
+    a = _ffi.Wba16Args()
+    a.dtype = dtype_id(x.dtype)
+    a.x, a.n, a.h, a.w, a.c, a.ldx = x.ptr, x.B, x.H, x.W, C, x.ld
+    a.out, a.ldo = out.ptr, out.ld
+    a.heads, a.ws, a.shift, a.mask_kind = heads, ws, shift, mask_kind
+    a.scale = scale
+    a.table, a.tab_sr, a.tab_sh = _dp(table), tab_sr, tab_sh
+    a.qkv_w, a.qkv_bias = _dp(qkv_pk.w), _dp(qkv_pk.bias)
+    check(_lib().lic_wba16_qkv_attn_fwd(ctypes.byref(a), stream_handle()))
+    return out
+
+
 def layernorm(x: Act, weight: torch.Tensor, bias: torch.Tensor, eps: float, out: Optional[Act] = None) -> Act:
     if out is None:
         out = Act.empty(x.B, x.H, x.W, x.c, x.dtype, x.t.device)

@@ -1,5 +1,4 @@
 """Conv helpers and Win_noShift_Attention (reference layers/layers.py:36-111)."""
-import os
 from typing import Optional
 
 import torch
@@ -44,28 +43,13 @@ class Win_noShift_Attention(nn.Module):
             wba(), conv1x1(N, N), wba(), ResidualBlock(N, N), conv3x3(N, N), wba(), ResidualBlock(N, N),
             conv7x7(N, N), wba(), ResidualBlock(N, N))
 
-    # maps up to this many pixels (batch x H x W) run conv_a concurrently with conv_b: there every
-    # launch is latency-bound (the 16x16 latents); on the big maps both chains fill the GPU alone
-    CONCURRENT_MAX_PIX = 16384
-
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
-        side = None
-        if (x.B * x.H * x.W <= self.CONCURRENT_MAX_PIX and os.environ.get("LIC_CONCURRENT_RU", "0") == "1" and
-                "wnsa" not in os.environ.get("LIC_DEBUG_SERIAL", "")):
-            ss = self.__dict__.setdefault("_lic_streams", {})
-            if str(x.t.device) not in ss:
-                ss[str(x.t.device)] = torch.cuda.Stream(device=x.t.device)
-            side = ss[str(x.t.device)]
-        main = torch.cuda.current_stream(x.t.device)
+        # (conv_a on a side stream, concurrent with conv_b, was tried on the 16x16 latents: a hipGraph
+        # capture of the slice loop's stream fork with this one nested in it segfaults in
+        # capture_end with plain torch kernels too -- tools/capture_fork_probe.py)
         a = x
-        if side is not None:   # joined before conv_b's last launch, which reads a
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                for blk in self.conv_a:
-                    a = blk.run(a)
-        else:
-            for blk in self.conv_a:
-                a = blk.run(a)
+        for blk in self.conv_a:
+            a = blk.run(a)
         b = self.conv_b[0].run(x)
         b = self.conv_b[1].run(b)
         b = self.conv_b[2].run(b)
@@ -75,8 +59,6 @@ class Win_noShift_Attention(nn.Module):
         b = self.conv_b[6].run(b)
         b = self.conv_b[7].run(b)
         b = self.conv_b[8].run(b)
-        if side is not None:
-            main.wait_stream(side)
         return self.conv_b[9].run(b, out, gate_a=a, gate_r=x)
 
     def forward(self, x):

@@ -20,6 +20,7 @@ __all__ = ["WindowAttention", "WinBasedAttention", "window_partition", "window_r
 
 _FUSED = os.environ.get("LIC_FUSED_WBA", "1") != "0"
 _FUSED_PROJ = os.environ.get("LIC_FUSED_WBA_PROJ", "0") == "1"
+_FUSED16 = os.environ.get("LIC_FUSED_WBA16", "1") != "0"
 
 
 def window_partition(x, window_size=8):
@@ -95,6 +96,12 @@ class WinBasedAttention(nn.Module):
                                 out=out if fuse_proj else None,
                                 proj_pk=self.attn.proj.packed(x.dtype) if fuse_proj else None)
             return a if fuse_proj else self.attn.proj.run(a, out, r1=x, **proj_kw)
+        if _FUSED16 and Fn.wba16_qkv_attn_ok(x, self.dim, self.num_heads, self.window_size):
+            # 16-bit: qkv + attention in one launch (csrc/wba16.hip); LIC_FUSED_WBA16=0 for two launches
+            a = Fn.wba16_qkv_attn(x, self.attn.qkv.packed(x.dtype), self.num_heads, self.window_size,
+                                  self.shift_size, self.attn.relative_position_bias_table, self.num_heads, 1,
+                                  1 if self.shift_size > 0 else 0, float(self.attn.scale))
+            return self.attn.proj.run(a, out, r1=x, **proj_kw)
         qkv = self.attn.qkv.run(x)
         a = Fn.win_attn(qkv, self.dim, self.num_heads, self.window_size, self.shift_size,
                         self.attn.relative_position_bias_table, self.num_heads, 1,

@@ -129,36 +129,15 @@ class SWAtten(AttentionBlock):
             self.in_conv = conv1x1(input_dim, inter_dim)
             self.out_conv = conv1x1(inter_dim, output_dim)
 
-    def _side(self, device):
-        """The stream conv_a runs on (None: serial unless LIC_CONCURRENT_RU=1, or LIC_DEBUG_SERIAL
-        containing 'swatten')."""
-        if os.environ.get("LIC_CONCURRENT_RU", "0") != "1" or "swatten" in os.environ.get("LIC_DEBUG_SERIAL", ""):
-            return None
-        ss = self.__dict__.setdefault("_lic_streams", {})
-        if str(device) not in ss:
-            ss[str(device)] = torch.cuda.Stream(device=device)
-        return ss[str(device)]
-
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
         x = self.in_conv.run(x)
-        # conv_a (3 ResidualUnits on x) is independent of the Swin chain that feeds conv_b until
-        # the gate: on the 16x16 latents both chains are latency-bound launches, so conv_a runs
-        # concurrently on a side stream (joined before the gate; every later use of that stream
-        # starts with a wait on this one, so its buffers are not reused early)
-        side = self._side(x.t.device)
-        main = torch.cuda.current_stream(x.t.device)
+        # conv_a (3 ResidualUnits on x) and the Swin chain that feeds conv_b run in order on the
+        # current stream: forking conv_a to a stream of its own nests that fork inside the slice
+        # loop's, and hipGraph capture of the nested fork segfaults (tools/capture_fork_probe.py)
         a = x
-        if side is not None:
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                for u in self.conv_a:
-                    a = u.run(a)
-        else:
-            for u in self.conv_a:
-                a = u.run(a)
+        for u in self.conv_a:
+            a = u.run(a)
         z = self.non_local_block.run(x)
-        if side is not None:
-            main.wait_stream(side)
         b = z
         for u in list(self.conv_b)[:3]:
             b = u.run(b)

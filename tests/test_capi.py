@@ -66,7 +66,7 @@ def test_ctypes_struct_offsets_match_c_compiler(tmp_path):
         pytest.skip("gcc not available")
     structs = {"lic_conv_args": _ffi.ConvArgs, "lic_attn_args": _ffi.AttnArgs,
                "lic_rate_args": _ffi.RateArgs, "lic_rans_args": _ffi.RansArgs, "lic_wgrad_args": _ffi.WgradArgs,
-               "lic_resunit_args": _ffi.ResunitArgs, "lic_wba_args": _ffi.WbaArgs}
+               "lic_resunit_args": _ffi.ResunitArgs, "lic_wba_args": _ffi.WbaArgs, "lic_wba16_args": _ffi.Wba16Args}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lic.h"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')

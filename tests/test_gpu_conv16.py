@@ -229,3 +229,146 @@ def test_gemm16_small_map_linear(dtype):
         out = m.to(DEV).run(_act(x, dtype)).nchw()
         ref = F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu())
         _check(out, ref, dtype, f"1x1 {ci}->{co} @16x16 {dtype}")
+
+
+# ---- conv16s (csrc/conv16s.h): 16-bit stride-1 3x3 / 7x7 on the small maps conv16 does not fill ----
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,B,H,W", [
+    (192, 192, 3, 32, 16, 16),    # Win_noShift_Attention 3x3 @ H/16 (the a_model's 13 latent-map 3x3s)
+    (192, 192, 7, 32, 16, 16),    # its conv7x7
+    (192, 192, 3, 2, 16, 16),     # few images: 32-channel blocks
+    (224, 128, 3, 32, 16, 16),    # slice-loop cc_mean / cc_scale first conv (64-channel blocks)
+    (336, 224, 3, 8, 16, 16),     # 21 input chunks: uneven per-wave chunk counts
+    (192, 192, 3, 4, 32, 32),     # a 32x32 map with too few tiles for conv16
+    (192, 192, 3, 3, 13, 21),     # ragged tiles (13 = 3*4+1 rows, 21 = 16+5 columns)
+    (192, 192, 7, 5, 9, 30),      # ragged 7x7
+    (128, 32, 3, 16, 16, 16),     # narrow output (one 32-channel block)
+])
+def test_conv16s_vs_torch_fp32(dtype, cin, cout, k, B, H, W):
+    from lic_amd.layers import Conv2d
+    torch.manual_seed(80 + k + cin)
+    m = Conv2d(cin, cout, k, 1, k // 2)
+    x = torch.randn(B, cin, H, W) * 0.5
+    out = m.to(DEV).run(_act(x, dtype)).nchw()
+    ref = F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 1, k // 2)
+    _check(out, ref, dtype, f"conv16s conv{k}x{k} {cin}->{cout} {dtype} B={B} {H}x{W}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_conv16s_epilogues_views_dual_store(dtype):
+    """The latent-map Win_noShift_Attention epilogues (LeakyReLU; + residual; the gate
+    g*sigmoid(lrelu(acc+b) + r1) + r2) on channel-window views with a second destination, and the
+    generic implicit-GEMM kernel on the same packed operands."""
+    from lic_amd.layers import Conv2d
+    from lic_amd.functional import Act
+    import lic_amd.functional as Fn
+    from lic_amd import _ffi as L
+    torch.manual_seed(62)
+    B, H, W, C = 32, 16, 16, 192
+    m = Conv2d(C, C, 3, 1, 1).to(DEV)
+    big = (torch.randn(B, H, W, 3 * C + 64, device=DEV) * 0.5).to(dtype)
+    X, R1, G = Act(big, 64, C), Act(big, 64 + C, C), Act(big, 64 + 2 * C, C)
+    R2 = Act(big, 0, C)
+
+    def nchw(view):
+        return view.t[..., view.c0:view.c0 + view.c].float().permute(0, 3, 1, 2).cpu()
+
+    base = F.conv2d(nchw(X), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 1, 1)
+    cases = [
+        (dict(act=L.ACT_LRELU), F.leaky_relu(base)),
+        (dict(act=L.ACT_LRELU, r1=R1), F.leaky_relu(base) + nchw(R1)),
+        (dict(act=L.ACT_LRELU, r1=R1, epi=L.EPI_GATE, g=G, r2=R2),
+         nchw(G) * torch.sigmoid(F.leaky_relu(base) + nchw(R1)) + nchw(R2)),
+    ]
+    for idx, (kw, ref) in enumerate(cases):
+        out_buf = torch.zeros(B, H, W, C + 96, device=DEV, dtype=dtype)
+        out2 = torch.zeros(B, H, W, C + 32, device=DEV, dtype=dtype)
+        m.run(X, out=Act(out_buf, 96, C), y2=Act(out2, 0, C), **kw)
+        _check(out_buf[..., 96:].permute(0, 3, 1, 2), ref, dtype, f"conv16s epilogue case {idx} {dtype}")
+        assert torch.equal(out_buf[..., 96:], out2[..., :C])
+        assert out_buf[..., :96].abs().sum().item() == 0 and out2[..., C:].abs().sum().item() == 0
+    pk = m.packed(dtype, (1, 1, 1, 1))
+    a = Fn.conv(X, pk).nchw().float()
+    b = Fn.conv(X, pk, force_generic=True).nchw().float()
+    assert (a - b).abs().max().item() <= TOL[dtype] * b.abs().max().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_gemm16_gdn_residual(dtype):
+    """GDN + skip (ResidualBlockWithStride, net_ga.py:68-86: gdn(conv2(...)) + skip(x)) as one launch:
+    the GDN epilogue with the residual operand."""
+    from lic_amd.layers import GDN
+    from lic_amd.functional import Act
+    import lic_amd.functional as Fn
+    from lic_amd._ffi import EPI_GDN_RSQRT, PRO_SQUARE
+    from oracle import ref_cpu as R
+    torch.manual_seed(75)
+    C = 192
+    m = GDN(C)
+    with torch.no_grad():
+        m.beta.add_(0.3 * torch.rand(C))
+        m.gamma.add_(0.05 * torch.rand(C, C))
+    m = m.to(DEV)
+    x = torch.randn(4, C, 128, 96) * 2
+    r = torch.randn(4, C, 128, 96)
+    out = Fn.gdn(_act(x, dtype), m.packed(dtype), EPI_GDN_RSQRT, None, _act(r, dtype)).nchw().float().cpu()
+    P = {"g." + k: v.detach().float().cpu() for k, v in m.state_dict().items()}
+    xr, rr = _rounded(x, dtype), _rounded(r, dtype)
+    ref = R.gdn_compressai(xr, P, "g") + rr
+    err = (out - ref).abs().max().item()
+    assert err <= (1e-2 if dtype == torch.float16 else 3e-2) * ref.abs().max().item(), err
+    # g another tensor than the input (the register-g variant does not apply): g * rsqrt(beta + gamma x^2) + r1
+    y = torch.randn(4, C, 128, 96)
+    out2 = Fn.conv(_act(x, dtype), m.packed(dtype), epi=EPI_GDN_RSQRT, g=_act(y, dtype), r1=_act(r, dtype),
+                   prologue=PRO_SQUARE).nchw().float().cpu()
+    beta = R.nnp_forward(P["g.beta"], P["g.beta_reparam.lower_bound.bound"], P["g.beta_reparam.pedestal"])
+    gamma = R.nnp_forward(P["g.gamma"], P["g.gamma_reparam.lower_bound.bound"], P["g.gamma_reparam.pedestal"])
+    ref2 = _rounded(y, dtype) * torch.rsqrt(F.conv2d(xr ** 2, gamma.reshape(C, C, 1, 1), beta)) + rr
+    err2 = (out2 - ref2).abs().max().item()
+    assert err2 <= (1e-2 if dtype == torch.float16 else 3e-2) * ref2.abs().max().item(), err2
+
+
+# ---- wba16 (csrc/wba16.hip): 16-bit qkv Linear + window attention in one launch ----
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W,shift", [(4, 64, 64, 4), (2, 32, 48, 0), (3, 16, 24, 4)])
+def test_wba16_matches_unfused(dtype, B, H, W, shift):
+    """The fused launch against the two-launch path (qkv Linear -> win_attn, whose own parity against
+    the oracle is tests/test_gpu_attn.py) on the same operands: WinBasedAttention, reference
+    layers/win_attention.py:85-116 + 154-209, with the region mask of the shifted windows at the last
+    window row / column; and the whole block (proj + shortcut) through the module."""
+    import lic_amd.functional as Fn
+    from lic_amd.functional import Act
+    from lic_amd.layers.win_attention import WinBasedAttention
+    torch.manual_seed(90 + H + shift)
+    m = WinBasedAttention(dim=192, num_heads=8, window_size=8, shift_size=shift).to(DEV)
+    with torch.no_grad():
+        m.attn.relative_position_bias_table.normal_(0, 0.5)
+    x = Act.from_nchw((torch.randn(B, 192, H, W) * 0.7).to(DEV), dtype)
+    att = m.attn
+    args = (8, 8, shift, att.relative_position_bias_table, 8, 1, 1 if shift > 0 else 0, float(att.scale))
+    fused = Fn.wba16_qkv_attn(x, att.qkv.packed(dtype), *args).nchw().float()
+    qkv = att.qkv.run(x)
+    unfused = Fn.win_attn(qkv, 192, 8, 8, shift, att.relative_position_bias_table, 8, 1, 1 if shift > 0 else 0,
+                          False, float(att.scale)).nchw().float()
+    scale = unfused.abs().max().item()
+    # same operands and rounding points; the qkv accumulation order differs (fp32 sums of 192 products)
+    assert (fused - unfused).abs().max().item() <= 2 * TOL[dtype] * scale
+    # the whole block (proj + shortcut) through the module against the three-launch path
+    blk = m.run(x).nchw().float()
+    ref_blk = att.proj.run(Act.from_nchw(unfused, dtype), r1=x).nchw().float()
+    assert (blk - ref_blk).abs().max().item() <= 4 * TOL[dtype] * ref_blk.abs().max().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_conv16_gelu_96(dtype):
+    """ResidualBottleneck's 3x3 96->96 + GELU (net_ga.py:89-103): conv16's 96-channel register epilogue."""
+    from lic_amd.layers import Conv2d
+    from lic_amd import _ffi as L
+    torch.manual_seed(63)
+    m = Conv2d(96, 96, 3, 1, 1)
+    x = torch.randn(32, 96, 64, 64) * 0.5
+    out = m.to(DEV).run(_act(x, dtype), act=L.ACT_GELU).nchw()
+    ref = F.gelu(F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 1, 1))
+    _check(out, ref, dtype, f"conv3x3 96->96 + GELU {dtype}")

@@ -1,5 +1,9 @@
 """hipGraph capture of nested stream fork / join patterns (the LIC_CONCURRENT_RU side streams).
 
+Finding (r05l): the nested pattern segfaults in capture_end with plain torch kernels and every
+capture_error_mode; flat and sibling forks capture and replay bit-exactly.  The nested side streams
+were removed from the model; tests/test_gpu_capture.py keeps the one-level forks the slice loop uses.
+
 Round 4 saw `bench.py` segfault inside torch.cuda.graphs.capture_end with LIC_CONCURRENT_RU=1: the
 slice loop forks its scale branch to a stream (net_ga._slice_loop) and, inside it, SWAtten forks its
 conv_a chain to a per-instance stream; Win_noShift_Attention (16x16 latents) does the same on the main
@@ -22,7 +26,9 @@ def conv_op(x):
     """One liblic launch (1x1 conv on the 16x16 latent shape) when the library is there, else a torch op."""
     import lic_amd.functional as Fn
     from lic_amd.layers import Conv2d
-    m = conv_op.__dict__.setdefault("m", Conv2d(128, 128, 1, 1, 0).cuda())
+    if "m" not in conv_op.__dict__:   # (created by the eager pass, before any capture)
+        conv_op.m = Conv2d(128, 128, 1, 1, 0).cuda()
+    m = conv_op.m
     return Fn.conv(Fn.Act(x), m.packed(x.dtype)).t
 
 

@@ -1,7 +1,5 @@
-# The GPU call of the moment (overwritten per call; results under gpurun_out/<tag>/).
-bash tools/gpu.sh r05k \
- 'c16tests|300|python -u -m pytest tests/test_gpu_conv16.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider' \
- 'cb16|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --only qkv1x1@64,proj1x1@64,gdn1x1@128,qkv1x1@16,gdn1x1@32' \
- 'bench16|300|python -u bench.py --precision fp16 --no-extras' \
- 'layers16|300|python -u tools/layer_profile.py --precision fp16 --what a_model' \
- 'probe|120|python -u tools/capture_fork_probe.py'
+bash tools/gpu.sh r05q \
+ 'c16tests|300|python -u -m pytest tests/test_gpu_conv16.py tests/test_gpu_attn.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider' \
+ 'gdn|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --gdn gdn --only gdn1x1@128,gdn1x1@32' \
+ 'cb7|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --only wnsa7x7@64,wnsa3x3@64' 'cb7off|120|env LIC_CONV16_7X7=0 python -u tools/conv_bench.py --dtype fp16 --auto-only --only wnsa7x7@64' 'bench16|300|python -u bench.py --precision fp16 --no-extras' \
+ 'profa|300|rocprofv3 --kernel-trace -d gpurun_out/r05q/prof_a -o run -- python3 bench.py --precision fp16 --profile --profile-a-model --steps 5 --warmup 1'
