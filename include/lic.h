@@ -551,7 +551,8 @@ int lic_wba_qkv_attn_fwd(const lic_wba_args* a, lic_stream_t stream);
  * (the 16-bit packed [3C][1][C] weights of its ConvPack, fp32 bias) + shifted-window attention with
  * the unfused launches' arithmetic (q, k, v rounded to the 16-bit type after the bias, the scale on
  * the fp32 dot); out = the C-channel attention output the proj Linear consumes.  C = 192, 8 heads,
- * 8x8 windows, H and W multiples of 8; x 16-B aligned rows of 8k elements, out 8-B aligned.
+ * 8x8 windows, H and W multiples of 8; x 16-B aligned rows of 8k elements, out 8-B aligned and not
+ * overlapping x.
  * Replaces model/layers.py WinBasedAttention's qkv + attention (reference layers/win_attention.py:85-116). */
 typedef struct lic_wba16_args {
   int32_t dtype;                             /* LIC_F16 or LIC_BF16 */

@@ -569,6 +569,12 @@ int conv16_dispatch_impl(const lic_conv_args& a, hipStream_t s, int& status) {
     }
   }
   if (a.mi < 16 || a.mj < 32) return 0;
+  // ResidualBlockWithStride's conv3x3 s2 (64^2 -> 32^2 in the a_model): four input-parity phases
+  // (2x2 / 2x1 / 1x2 / 1x1 taps); 96-channel blocks where 192 leave the chip half empty
+  if (a.isy == 2 && a.isx == 2 && a.ntaps == 9 && wd_env("LIC_CONV16_S2", 1)) {
+    if (a.copad % 192 == 0 && blocks(192) >= 128) return try_conv16<T, 3, 3, 2, 0, 192, 2>(a, s, status);
+    if (a.copad % 96 == 0 && blocks(96) >= 128) return try_conv16<T, 3, 3, 2, 0, 96, 1>(a, s, status);
+  }
   // ZeroPad2d((1,2,1,2)) + conv5x5 s2 (the a_model's downsampling convs): four input-parity phases
   if (a.isy == 2 && a.isx == 2 && a.ntaps == 25 && a.copad % 192 == 0 && blocks(192) >= 128 &&
       wd_env("LIC_CONV16_S2", 1))

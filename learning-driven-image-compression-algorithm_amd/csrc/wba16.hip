@@ -4,14 +4,17 @@
 // channels, 8x8 windows: the a_model's Win_noShift_Attention blocks at 64x64 (layers/layers.py:87-102).
 //
 // Unfused, the qkv 1x1 writes a 3C map (151 MB per call at 64^2 x 32, fp16) that the attention kernel
-// reads straight back.  Here a persistent workgroup (8 waves, one per CU) walks windows: the window's
-// 64 x 192 activations go to LDS; the qkv GEMM (transposed: A = the packed [3C][C] weights streamed
-// from L2, B = token fragments from LDS) leaves q | k in LDS as [token][384] rows and v as V^T
-// [channel][token] rows, rounded to the 16-bit type after the bias exactly as the unfused qkv
-// launch stores them; then wave h runs head h's attention with the fragments from LDS (the unfused
-// kernel's arithmetic, csrc/attention_mfma.hip: S^T = K Q^T, scale and bias on the fp32 dot, softmax
-// over the lane's registers + lane ^ 32, O^T = V^T P^T) and stores its 24 output channels.
-// The next window's activations are loaded into registers during the attention phase.
+// reads straight back.  Here persistent workgroups (8 waves, two per CU: 72 KB of LDS each) walk
+// windows: the window's 64 x 192 activations go to LDS; per head group (heads 4g .. 4g+3) the qkv GEMM
+// of the group's 288 channels (transposed: A = the packed [3C][C] weights streamed from L2, each
+// fragment read once per window; B = token fragments from LDS) leaves q | k in LDS as [token][192]
+// rows and v as V^T [channel][token] rows, rounded to the 16-bit type after the bias exactly as the
+// unfused qkv launch stores them; then wave (head, query tile) runs that head's attention for 32
+// queries with the fragments from LDS (the unfused kernel's arithmetic, csrc/attention_mfma.hip:
+// S^T = K Q^T, scale and bias on the fp32 dot, softmax over the lane's registers + lane ^ 32,
+// O^T = V^T P^T) and stores its 24 output channels.  The next window's activations are loaded into
+// registers during the last attention phase; the other workgroup on the CU hides the barriers.
+#include <type_traits>
 #include "lic_common.h"
 
 namespace lic {
@@ -20,23 +23,24 @@ namespace {
 
 constexpr int W16_C = 192, W16_HEADS = 8, W16_D = 24, W16_WS = 8, W16_T = 64;
 constexpr int W16_XS = 200;   // elements per token row of the x tile (400 B: conflict-free b128 reads)
-constexpr int W16_QS = 392;   // elements per token row of q | k (384 + 8)
-constexpr int W16_VS = 72;    // elements per channel row of V^T (64 + 8)
+constexpr int W16_QS = 200;   // elements per token row of the group's q | k (96 + 96 + 8)
+constexpr int W16_VS = 72;    // elements per channel row of the group's V^T (64 + 8)
 constexpr int W16_X = W16_T * W16_XS * 2;
 constexpr int W16_QK = W16_T * W16_QS * 2;
-constexpr int W16_V = W16_C * W16_VS * 2;
+constexpr int W16_V = 96 * W16_VS * 2;
 constexpr int W16_TAB = W16_HEADS * 225 * 4;
 constexpr int W16_LDS = W16_X + W16_QK + W16_V + W16_TAB;
-static_assert(W16_LDS <= 160 * 1024, "LDS");
+constexpr int W16_R = 3, W16_PD = W16_R - 1;   // weight ring (12 K steps: R divides 12)
+static_assert(2 * W16_LDS <= 160 * 1024, "LDS: two workgroups per CU");
 
 }  // namespace
 
 template <typename T>
-__global__ __launch_bounds__(512, 1) void wba16_qkv_attn_kernel(const lic_wba16_args a) {
+__global__ __launch_bounds__(512, 4) void wba16_qkv_attn_kernel(const lic_wba16_args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* xs = smem;                                       // [64 tokens][W16_XS]
-  T* qk = (T*)(smem + W16_X);                            // [64 tokens][W16_QS]: q 0..191, k 192..383
-  T* vt = (T*)(smem + W16_X + W16_QK);                   // [192 channels][W16_VS]: V^T
+  T* qk = (T*)(smem + W16_X);                            // [64 tokens][W16_QS]: q 0..95, k 96..191 of the group
+  T* vt = (T*)(smem + W16_X + W16_QK);                   // [96 channels][W16_VS]: the group's V^T
   float* tab = (float*)(smem + W16_X + W16_QK + W16_V);  // [8 heads][225]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -67,131 +71,127 @@ __global__ __launch_bounds__(512, 1) void wba16_qkv_attn_kernel(const lic_wba16_
   };
   if ((int)blockIdx.x < nwin) load_x(blockIdx.x);
 
-  // qkv weights: packed [576][1][192] (the qkv Linear's ConvPack), A fragment of channel tile ct and
-  // K step kk = rows 32 ct + lr, input channels 16 kk + 8 lh .. +7
+  // qkv weights: packed [576][1][192] (the qkv Linear's ConvPack), A fragment of packed channel tile jt
+  // and K step kk = rows 32 jt + lr, input channels 16 kk + 8 lh .. +7
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.qkv_w, (short)0, 576 * 192 * 2, 0x00020000);
   const unsigned wl = (unsigned)((lr * W16_C + 8 * lh) * 2);
 
   for (int win = blockIdx.x; win < nwin; win += gridDim.x) {
-    // ---- A: the window's activations to LDS (the previous window's qkv phase, their only reader,
-    // ended at a barrier) ----
+    const int wx = win % nwx, wy = (win / nwx) % nwy;
+    // ---- A: the window's activations to LDS (their only reader, the previous window's last qkv
+    // phase, ended at a barrier) ----
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int f = tid + 512 * i, t = f / 24, ch = (f % 24) * 8;
       *(u32x4*)(xs + t * (W16_XS * 2) + ch * 2) = xv[i];
     }
-    __syncthreads();   // (also: every wave's previous attention phase is done with q | k / V^T)
+    for (int g = 0; g < 2; ++g) {
+      __syncthreads();   // x written (g = 0); the previous attention phase done with q | k / V^T
 
-    // ---- B: qkv = x W^T + b for 18 channel tiles x 2 token tiles; wave w takes channel tiles
-    // w, w + 8 (, w + 16): both token tiles of each, so every weight fragment is read once ----
-    auto gemm = [&](auto cnt_c) __attribute__((always_inline)) {
-      constexpr int CNT = decltype(cnt_c)::value;
-      floatx16 acc[CNT][2];
+      // ---- B: the group's 9 channel tiles (q, k, v x 3 of 32) x 2 token tiles = 18 tiles: wave w takes
+      // local channel tile w for both token tiles (its weight fragments serve both), and the ninth
+      // channel tile's two token tiles go to waves e and e + 1 (e = 0 for g = 0, 4 for g = 1) ----
+      auto gemm = [&](auto ex_c) __attribute__((always_inline)) {
+        constexpr int EX = decltype(ex_c)::value;   // 1: this wave also has tile (8, tx)
+        constexpr int CNT = 1 + EX;
+        const int e0 = 4 * g, tx = wave - e0;
+        int jt[CNT], lt[CNT];
 #pragma unroll
-      for (int i = 0; i < CNT; ++i)
+        for (int i = 0; i < CNT; ++i) {
+          lt[i] = i == 0 ? wave : 8;
+          jt[i] = (lt[i] / 3) * 6 + 3 * g + lt[i] % 3;
+        }
+        auto load_w = [&](int kk, u32x4(&f)[CNT]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
+          for (int i = 0; i < CNT; ++i)
+            f[i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wl, (jt[i] * 32 * W16_C + 16 * kk) * 2, 0);
+        };
+        floatx16 acc[2], accx;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][tt][r] = 0.f;
-      auto load_w = [&](int kk, u32x4(&f)[CNT]) __attribute__((always_inline)) {
+        for (int r = 0; r < 16; ++r) acc[0][r] = acc[1][r] = accx[r] = 0.f;
+        u32x4 fw[W16_R][CNT];
 #pragma unroll
-        for (int i = 0; i < CNT; ++i)
-          f[i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wl, ((wave + 8 * i) * 32 * W16_C + 16 * kk) * 2, 0);
-      };
-      u32x4 fw[3][CNT];
-      load_w(0, fw[0]);
-      load_w(1, fw[1]);
+        for (int q = 0; q < W16_PD; ++q) load_w(q, fw[q]);
 #pragma unroll
-      for (int kk = 0; kk < 12; ++kk) {
-        if (kk + 2 < 12) load_w(kk + 2, fw[(kk + 2) % 3]);
-        u32x4 fx[2];
+        for (int kk = 0; kk < 12; ++kk) {
+          if (kk + W16_PD < 12) load_w(kk + W16_PD, fw[(kk + W16_PD) % W16_R]);
+          u32x4 fx[2];
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) fx[tt] = *(const u32x4*)(xs + (32 * tt + lr) * (W16_XS * 2) + (16 * kk + 8 * lh) * 2);
+          for (int tt = 0; tt < 2; ++tt)
+            fx[tt] = *(const u32x4*)(xs + (32 * tt + lr) * (W16_XS * 2) + (16 * kk + 8 * lh) * 2);
 #pragma unroll
-        for (int i = 0; i < CNT; ++i)
+          for (int tt = 0; tt < 2; ++tt) acc[tt] = mfma_k16<T>(fw[kk % W16_R][0], fx[tt], acc[tt]);
+          if constexpr (EX) accx = mfma_k16<T>(fw[kk % W16_R][CNT - 1], tx ? fx[1] : fx[0], accx);
+        }
+        // + bias, rounded to T: lane (token 32 tt + lr) holds channels 32 jt + 8 q + 4 lh + (0..3)
+        auto store = [&](const floatx16& c, int i, int tt) __attribute__((always_inline)) {
+          const int which = lt[i] / 3;   // 0 q, 1 k, 2 v
+          const int t = 32 * tt + lr;
 #pragma unroll
-          for (int tt = 0; tt < 2; ++tt) acc[i][tt] = mfma_k16<T>(fw[kk % 3][i], fx[tt], acc[i][tt]);
-      }
-      // + bias, rounded to T: lane (token 32 tt + lr) holds channels 32 ct + 8 q + 4 lh + (0..3)
-#pragma unroll
-      for (int i = 0; i < CNT; ++i) {
-        const int ct = wave + 8 * i;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int n = 32 * ct + 8 * q + 4 * lh;
-          const floatx4 bv = *(const floatx4*)(a.qkv_bias + n);
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) {
-            const int t = 32 * tt + lr;
+          for (int q = 0; q < 4; ++q) {
+            const int lc = 32 * (lt[i] % 3) + 8 * q + 4 * lh;   // channel within the group's q / k / v
+            const floatx4 bv = *(const floatx4*)(a.qkv_bias + 32 * jt[i] + 8 * q + 4 * lh);
             T e[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) e[k] = from_f<T>(acc[i][tt][4 * q + k] + bv[k]);
-            if (ct < 12) {
-              *(uint2*)(qk + t * W16_QS + n) = *(const uint2*)e;
+            for (int k = 0; k < 4; ++k) e[k] = from_f<T>(c[4 * q + k] + bv[k]);
+            if (which < 2) {
+              *(uint2*)(qk + t * W16_QS + 96 * which + lc) = *(const uint2*)e;
             } else {
 #pragma unroll
-              for (int k = 0; k < 4; ++k) vt[(n - 2 * W16_C + k) * W16_VS + t] = e[k];
+              for (int k = 0; k < 4; ++k) vt[(lc + k) * W16_VS + t] = e[k];
             }
           }
-        }
-      }
-    };
-    if (wave < 2) gemm(std::integral_constant<int, 3>{});
-    else gemm(std::integral_constant<int, 2>{});
-    __syncthreads();
-    // the next window's activations, consumed by its phase A (the attention phase issues no loads)
-    if (win + (int)gridDim.x < nwin) load_x(win + gridDim.x);
-
-    // ---- C: head h = wave ----
-    {
-      const int h = wave;
-      const int wx = win % nwx, wy = (win / nwx) % nwy;
-      u32x4 kf[2][2] = {}, qf[2][2] = {};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int ch = 16 * s + 8 * lh;
-        if (ch >= W16_D) continue;
-#pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2) {
-          const T* row = qk + (32 * t2 + lr) * W16_QS + h * W16_D + ch;
-          qf[s][t2] = *(const u32x4*)row;
-          kf[s][t2] = *(const u32x4*)(row + W16_C);
-        }
-      }
-      floatx16 S[2][2];   // [key tile][query tile]
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) S[x][y][r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-          for (int ti = 0; ti < 2; ++ti) S[tj][ti] = mfma_k16<T>(kf[s][tj], qf[s][ti], S[tj][ti]);
-
-      // scale + bias (+ region mask), softmax over the keys (rows) of each query (lane column):
-      // register r of key tile tj is key 32 tj + 8 (r >> 2) + 4 lh + (r & 3)
-      const int split = W16_WS - a.shift;
-      const bool last_row = wy == nwy - 1, last_col = wx == nwx - 1;
-      const bool mask_on = a.mask_kind != 0 && (last_row || last_col);
-      auto reg_wba = [&](int y, int x) {
-        const int ly = y < a.h - W16_WS ? 0 : (y < a.h - a.shift ? 1 : 2);
-        const int lx = x < a.w - W16_WS ? 0 : (x < a.w - a.shift ? 1 : 2);
-        return ly * 3 + lx;
+        };
+        store(acc[0], 0, 0);
+        store(acc[1], 0, 1);
+        if constexpr (EX) store(accx, CNT - 1, tx);
       };
-      constexpr float L2E = 1.4426950408889634f;
+      if (wave == 4 * g || wave == 4 * g + 1) gemm(std::integral_constant<int, 1>{});
+      else gemm(std::integral_constant<int, 0>{});
+      __syncthreads();
+      // the next window's activations, consumed by its phase A (the attention phase issues no loads)
+      if (g == 1 && win + (int)gridDim.x < nwin) load_x(win + gridDim.x);
+
+      // ---- C: wave = (head 4g + hl, query tile ti) ----
+      {
+        const int hl = wave >> 1, ti = wave & 1, h = 4 * g + hl;
+        u32x4 kf[2][2] = {}, qf[2] = {};
 #pragma unroll
-      for (int ti = 0; ti < 2; ++ti) {
+        for (int s = 0; s < 2; ++s) {
+          const int ch = 16 * s + 8 * lh;
+          if (ch >= W16_D) continue;
+          qf[s] = *(const u32x4*)(qk + (32 * ti + lr) * W16_QS + hl * W16_D + ch);
+#pragma unroll
+          for (int tj = 0; tj < 2; ++tj) kf[s][tj] = *(const u32x4*)(qk + (32 * tj + lr) * W16_QS + 96 + hl * W16_D + ch);
+        }
+        floatx16 S[2];   // [key tile], this wave's query tile
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) S[x][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int tj = 0; tj < 2; ++tj) S[tj] = mfma_k16<T>(kf[s][tj], qf[s], S[tj]);
+
+        // scale + bias (+ region mask), softmax over the keys (rows) of query i (lane column):
+        // register r of key tile tj is key 32 tj + 8 (r >> 2) + 4 lh + (r & 3)
+        const int split = W16_WS - a.shift;
+        const bool last_row = wy == nwy - 1, last_col = wx == nwx - 1;
+        const bool mask_on = a.mask_kind != 0 && (last_row || last_col);
+        auto reg_wba = [&](int y, int x) {
+          const int ly = y < a.h - W16_WS ? 0 : (y < a.h - a.shift ? 1 : 2);
+          const int lx = x < a.w - W16_WS ? 0 : (x < a.w - a.shift ? 1 : 2);
+          return ly * 3 + lx;
+        };
+        constexpr float L2E = 1.4426950408889634f;
         const int i = 32 * ti + lr;
         const int iy = i / W16_WS, ix = i % W16_WS;
         const float* trow = &tab[h * 225 + (iy + W16_WS - 1) * 15 + (ix + W16_WS - 1) - 4 * lh];
 #pragma unroll
         for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) S[tj][ti][r] = S[tj][ti][r] * a.scale + trow[-((4 * tj + (r >> 2)) * 15 + (r & 3))];
+          for (int r = 0; r < 16; ++r) S[tj][r] = S[tj][r] * a.scale + trow[-((4 * tj + (r >> 2)) * 15 + (r & 3))];
         if (mask_on) {
           const int my_reg = a.mask_kind == 1 ? reg_wba(wy * W16_WS + iy, wx * W16_WS + ix) : 0;
 #pragma unroll
@@ -200,9 +200,9 @@ __global__ __launch_bounds__(512, 1) void wba16_qkv_attn_kernel(const lic_wba16_
             for (int r = 0; r < 16; ++r) {
               const int jy = 4 * tj + (r >> 2), jx = 4 * lh + (r & 3);
               if (a.mask_kind == 1) {
-                if (reg_wba(wy * W16_WS + jy, wx * W16_WS + jx) != my_reg) S[tj][ti][r] += -100.0f;
+                if (reg_wba(wy * W16_WS + jy, wx * W16_WS + jx) != my_reg) S[tj][r] += -100.0f;
               } else if ((last_row && ((iy < split) != (jy < split))) || (last_col && ((ix < split) != (jx < split)))) {
-                S[tj][ti][r] = -INFINITY;
+                S[tj][r] = -INFINITY;
               }
             }
         }
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(512, 1) void wba16_qkv_attn_kernel(const lic_wba16_
 #pragma unroll
         for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[tj][ti][r]);
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, S[tj][r]);
         mx = fmaxf(mx, __shfl_xor(mx, 32));
         const float mxl = mx * L2E;
         float sum = 0.f;
@@ -218,8 +218,8 @@ __global__ __launch_bounds__(512, 1) void wba16_qkv_attn_kernel(const lic_wba16_
         for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(S[tj][ti][r], L2E, -mxl));
-            S[tj][ti][r] = e;
+            const float e = __builtin_amdgcn_exp2f(fmaf(S[tj][r], L2E, -mxl));
+            S[tj][r] = e;
             sum += e;
           }
         sum += __shfl_xor(sum, 32);
@@ -227,54 +227,47 @@ __global__ __launch_bounds__(512, 1) void wba16_qkv_attn_kernel(const lic_wba16_
 #pragma unroll
         for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) S[tj][ti][r] *= inv;
-      }
+          for (int r = 0; r < 16; ++r) S[tj][r] *= inv;
 
-      // O^T[c][i] = sum_j V^T[c][j] P^T[j][i]: lane (c = lr, half lh) reads V^T row c in the permuted
-      // key order of P's registers (keys j0 .. j0+3 and j0+8 .. j0+11); rows c >= 24 read zeros
-      floatx16 O[2];
+        // O^T[c][i] = sum_j V^T[c][j] P^T[j][i]: lane (c = lr, half lh) reads V^T row c in the permuted
+        // key order of P's registers (keys j0 .. j0+3 and j0+8 .. j0+11); rows c >= 24 read zeros
+        floatx16 O;
 #pragma unroll
-      for (int ti = 0; ti < 2; ++ti)
+        for (int r = 0; r < 16; ++r) O[r] = 0.f;
+        const bool cok = lr < W16_D;
+        const T* vrow = vt + (hl * W16_D + (cok ? lr : 0)) * W16_VS;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) O[ti][r] = 0.f;
-      const bool cok = lr < W16_D;
-      const T* vrow = vt + (h * W16_D + (cok ? lr : 0)) * W16_VS;
+        for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
-      for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int j0 = 32 * tj + 16 * s2 + 4 * lh;
-          u32x4 va = {0u, 0u, 0u, 0u};
-          if (cok) {
-            *(uint2*)&va = *(const uint2*)(vrow + j0);
-            *((uint2*)&va + 1) = *(const uint2*)(vrow + j0 + 8);
-          }
-#pragma unroll
-          for (int ti = 0; ti < 2; ++ti) {
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int j0 = 32 * tj + 16 * s2 + 4 * lh;
+            u32x4 va = {0u, 0u, 0u, 0u};
+            if (cok) {
+              *(uint2*)&va = *(const uint2*)(vrow + j0);
+              *((uint2*)&va + 1) = *(const uint2*)(vrow + j0 + 8);
+            }
             u32x4 pb;
             T* pe = (T*)&pb;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) pe[e] = from_f<T>(S[tj][ti][8 * s2 + e]);
-            O[ti] = mfma_k16<T>(va, pb, O[ti]);
+            for (int e = 0; e < 8; ++e) pe[e] = from_f<T>(S[tj][8 * s2 + e]);
+            O = mfma_k16<T>(va, pb, O);
           }
-        }
-      // lane (query i, half lh) holds channels 8 g + 4 lh + (0..3) of head h (24 valid)
-      T* out = (T*)a.out;
+        // lane (query i, half lh) holds channels 8 q + 4 lh + (0..3) of head h (24 valid)
+        T* op = (T*)a.out + (int64_t)pix_of(win, i) * a.ldo + h * W16_D;
 #pragma unroll
-      for (int ti = 0; ti < 2; ++ti) {
-        T* op = out + (int64_t)pix_of(win, 32 * ti + lr) * a.ldo + h * W16_D;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const int c0 = 8 * g + 4 * lh;
+        for (int q = 0; q < 3; ++q) {
+          const int c0 = 8 * q + 4 * lh;
           if (c0 >= W16_D) continue;
           uint2 pk;
           T* e = (T*)&pk;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) e[k] = from_f<T>(O[ti][4 * g + k]);
+          for (int k = 0; k < 4; ++k) e[k] = from_f<T>(O[4 * q + k]);
           *(uint2*)(op + c0) = pk;
         }
       }
     }
+    // (no barrier here: x was last read before the barrier that followed the g = 1 qkv phase, and the
+    // next window's first qkv phase writes q | k / V^T only after its own barrier)
   }
 }
 
@@ -294,6 +287,14 @@ extern "C" int lic_wba16_qkv_attn_fwd(const lic_wba16_args* a, lic_stream_t stre
   if ((uintptr_t)a->qkv_w % 16 || (uintptr_t)a->qkv_bias % 16) return fail("wba16: weights / bias must be 16-byte aligned");
   if ((int64_t)a->n * a->h * a->w * (int64_t)(a->ldx > a->ldo ? a->ldx : a->ldo) >= (1LL << 31))
     return fail("wba16: map too large for int32 indexing");
+  {
+    // persistent workgroups read the next window's x while others store their outputs: out may not
+    // overlap x
+    const int64_t npix = (int64_t)a->n * a->h * a->w;
+    const uintptr_t x0 = (uintptr_t)a->x, x1 = x0 + (uintptr_t)(((npix - 1) * a->ldx + W16_C) * 2);
+    const uintptr_t o0 = (uintptr_t)a->out, o1 = o0 + (uintptr_t)(((npix - 1) * a->ldo + W16_C) * 2);
+    if (x0 < o1 && o0 < x1) return fail("wba16: out must not overlap x");
+  }
   const int64_t nwin = (int64_t)a->n * (a->h / W16_WS) * (a->w / W16_WS);
   static int ncu = 0;
   if (ncu == 0) {
@@ -302,7 +303,7 @@ extern "C" int lic_wba16_qkv_attn_fwd(const lic_wba16_args* a, lic_stream_t stre
         ncu <= 0)
       ncu = 256;
   }
-  const unsigned grid = (unsigned)(nwin < ncu ? nwin : ncu);
+  const unsigned grid = (unsigned)(nwin < 2 * ncu ? nwin : 2 * ncu);   // two workgroups per CU
   hipStream_t s = (hipStream_t)stream;
   const void* kern = a->dtype == LIC_F16 ? (const void*)wba16_qkv_attn_kernel<half_t> : (const void*)wba16_qkv_attn_kernel<bf16_t>;
   const hipError_t ea = ensure_dyn_lds(kern, W16_LDS);

@@ -96,10 +96,10 @@ def _compare_forward(arch, B, S, seed, xseed, precisions=("fp32", "fp32x6")):
     ref = R.net_forward(x, P, arch=arch)
     res = {p: _check_precision(arch, p, B, S, net0, x, ref, P) for p in precisions}
     masks = {p: r[0] for p, r in res.items()}
-    check_x6_rate_not_worse({p: r[1] for p, r in res.items()})
     if "fp32" in masks and "fp32x6" in masks:
         n = check_flip_sets_match(masks["fp32x6"], masks["fp32"], ref)
         print(f"flip-set difference fp32x6 vs exact fp32: {n}")
+    check_x6_rate_not_worse({p: r[1] for p, r in res.items()})   # last: may end the test as an xfail
 
 
 def test_cfg2_forward_b32_fp32_bit_exact_symbols():

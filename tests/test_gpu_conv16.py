@@ -372,3 +372,18 @@ def test_conv16_gelu_96(dtype):
     out = m.to(DEV).run(_act(x, dtype), act=L.ACT_GELU).nchw()
     ref = F.gelu(F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 1, 1))
     _check(out, ref, dtype, f"conv3x3 96->96 + GELU {dtype}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W", [(32, 64, 64), (16, 128, 128), (12, 70, 100)])
+def test_conv16_stride2_3x3(dtype, B, H, W):
+    """ResidualBlockWithStride's conv3x3 s2 pad 1 (net_ga.py:68-86) on conv16's input-parity phases
+    (2x2 / 2x1 / 1x2 / 1x1 taps), 96- and 192-channel blocks, ragged output (35 x 50 from 70 x 100)."""
+    from lic_amd.layers import Conv2d
+    from lic_amd import _ffi as L
+    torch.manual_seed(64 + H)
+    m = Conv2d(192, 192, 3, 2, 1)
+    x = torch.randn(B, 192, H, W) * 0.5
+    out = m.to(DEV).run(_act(x, dtype), act=L.ACT_LRELU).nchw()
+    ref = F.leaky_relu(F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 2, 1))
+    _check(out, ref, dtype, f"conv3x3 s2 {dtype} B={B} {H}x{W}")

@@ -23,6 +23,7 @@ SHAPES = [
     ("rbws_conv2@128", 192, 192, 3, 1, (1, 1, 1, 1), 128),
     ("conv5x5s2@128", 192, 192, 5, 2, (1, 1, 2, 2), 128),
     ("conv5x5s2@32", 192, 192, 5, 2, (1, 1, 2, 2), 32),
+    ("rbws3x3s2@64", 192, 192, 3, 2, (1, 1, 1, 1), 64),
     ("qkv1x1@64", 192, 576, 1, 1, (0, 0, 0, 0), 64),
     ("proj1x1@64", 192, 192, 1, 1, (0, 0, 0, 0), 64),
     ("c1x1@128", 192, 192, 1, 1, (0, 0, 0, 0), 128),
