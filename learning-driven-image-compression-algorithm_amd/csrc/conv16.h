@@ -223,6 +223,8 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
       (unsigned)(((lane >> 1) * a.ntaps * a.cpad + (((lane & 1) ^ ((lane >> 4) & 1)) * 8)) * 2);
   const int wrow_bytes = a.ntaps * a.cpad * 2;   // one output channel's packed weights
 
+  // (a chunk order rotated per workgroup, so that the workgroups sharing an L2 stream different weight
+  // lines, measured 0.3-2 % slower: r05w)
   auto issue_piece = [&](int m, int k, int g, int hb, int wb, bool with_halo) {
     // m < HPW: halo piece m; else weight piece m - HPW
     if (m < HPW) {
@@ -379,7 +381,12 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
     // back as 16 B of consecutive channels per lane and stored.  Unrolled per tile with compile-time
     // accumulator indices and ~50 instructions a tile (the general epilogue spends ~250 a tile).
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    char* stg = smem + wave * (32 * 80);   // 32 rows of 64 B, padded to 80 B (conflict-free b64 writes)
+    // one tile row (CT tiles = the wave's 96 channels) at a time: staged as [32 px][CT*32 ch] 16-bit rows
+    // (208-B pitch), ONE LDS round trip per row, then each pixel's CT*64 contiguous bytes stored as 16-B
+    // chunks (a round trip per tile made the epilogue 16 % of the kernel: profiles/r05 stamps)
+    constexpr int SP = 208;   // >= CT*64 + 16
+    static_assert(CT * 64 + 16 <= SP && NW * 32 * SP <= Geo::LDS_MAIN, "epilogue staging");
+    char* stg = smem + wave * (32 * SP);
     T* __restrict__ yg = (T*)a.y;
     T* __restrict__ y2g = (T*)a.y2;
     const T* __restrict__ r1g = (const T*)a.r1;
@@ -387,71 +394,75 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
     const T* __restrict__ r2g = (const T*)a.r2;
     const int act = a.act;
     const float slope = a.slope;
-    c16_static_for<0, CT * PJ>([&](auto qc) {
-      constexpr int q = decltype(qc)::value, i = q % CT, j = q / CT;
+    c16_static_for<0, PJ>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
       const int row = i0 + wr * PJ + j;
-      const int nloc = wc * Geo::WCH + i * 32;       // channel of the tile's first column, in the block
-      // residual / gate operands, in the accumulator layout (8 B = 4 channels per lane and run)
-      u32x2 rr[4], rg[4], r2v[4];
-      if (FAST == 2 || r1g) {
-        const int col = j0 + l32;
-        const bool ok = row < a.mi && col < a.mj;
-        const int64_t pix = ok ? ((int64_t)b * a.ho + a.oy0 + a.osy * row) * a.wo + a.ox0 + a.osx * col : 0;
-        const int nb = n0 + nloc + 4 * lh;
-        if (r1g) {
+      c16_static_for<0, CT>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const int nloc = wc * Geo::WCH + i * 32;       // channel of the tile's first column, in the block
+        // residual / gate operands, in the accumulator layout (8 B = 4 channels per lane and run)
+        u32x2 rr[4], rg[4], r2v[4];
+        if (FAST == 2 || r1g) {
+          const int col = j0 + l32;
+          const bool ok = row < a.mi && col < a.mj;
+          const int64_t pix = ok ? ((int64_t)b * a.ho + a.oy0 + a.osy * row) * a.wo + a.ox0 + a.osx * col : 0;
+          const int nb = n0 + nloc + 4 * lh;
+          if (r1g) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) rr[k] = *(const u32x2*)(r1g + pix * a.ldr1 + nb + 8 * k);
-        }
-        if constexpr (FAST == 2) {
+            for (int k = 0; k < 4; ++k) rr[k] = *(const u32x2*)(r1g + pix * a.ldr1 + nb + 8 * k);
+          }
+          if constexpr (FAST == 2) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            rg[k] = *(const u32x2*)(gg + pix * a.ldg + nb + 8 * k);
-            r2v[k] = *(const u32x2*)(r2g + pix * a.ldr2 + nb + 8 * k);
+            for (int k = 0; k < 4; ++k) {
+              rg[k] = *(const u32x2*)(gg + pix * a.ldg + nb + 8 * k);
+              r2v[k] = *(const u32x2*)(r2g + pix * a.ldr2 + nb + 8 * k);
+            }
           }
         }
-      }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const floatx4 bv = *(const floatx4*)(sbias + nloc + 8 * k + 4 * lh);
-        float w[4];
+        for (int k = 0; k < 4; ++k) {
+          const floatx4 bv = *(const floatx4*)(sbias + nloc + 8 * k + 4 * lh);
+          float w[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = acc[i][j][4 * k + e] + bv[e];
-        if (act == LIC_ACT_LRELU) {
+          for (int e = 0; e < 4; ++e) w[e] = acc[i][j][4 * k + e] + bv[e];
+          if (act == LIC_ACT_LRELU) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : w[e] * slope;
-        } else if (act == LIC_ACT_RELU) {
+            for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : w[e] * slope;
+          } else if (act == LIC_ACT_RELU) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : 0.f;
-        } else if (BN == 96 && act == LIC_ACT_GELU) {   // (ResidualBottleneck's 3x3; 4 tiles a wave)
+            for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : 0.f;
+          } else if (BN == 96 && act == LIC_ACT_GELU) {   // (ResidualBottleneck's 3x3; 4 tiles a wave)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] = gelu_f(w[e]);
+            for (int e = 0; e < 4; ++e) w[e] = gelu_f(w[e]);
+          }
+          if (r1g) {
+            const T* re = (const T*)&rr[k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] += to_f(re[e]);
+          }
+          if constexpr (FAST == 2) {   // gate: g * sigmoid(.) + r2
+            const T* ge = (const T*)&rg[k];
+            const T* r2e = (const T*)&r2v[k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = to_f(ge[e]) * sigmoid_f(w[e]) + to_f(r2e[e]);
+          }
+          u32x2 raw;
+          T* o = (T*)&raw;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = from_f<T>(w[e]);
+          *(u32x2*)(stg + l32 * SP + (i * 32 + 8 * k + 4 * lh) * 2) = raw;
         }
-        if (r1g) {
-          const T* re = (const T*)&rr[k];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] += to_f(re[e]);
-        }
-        if constexpr (FAST == 2) {   // gate: g * sigmoid(.) + r2
-          const T* ge = (const T*)&rg[k];
-          const T* r2e = (const T*)&r2v[k];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] = to_f(ge[e]) * sigmoid_f(w[e]) + to_f(r2e[e]);
-        }
-        u32x2 raw;
-        T* o = (T*)&raw;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = from_f<T>(w[e]);
-        *(u32x2*)(stg + l32 * 80 + (8 * k + 4 * lh) * 2) = raw;
-      }
+      });
       wave_lds_sync();
+      constexpr int NCH = CT * 4;   // 16-B chunks of a pixel's CT*32 channels
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int idx = lane + 64 * h, pr = idx >> 2, c4 = idx & 3;   // pixel of the tile row, 16-B chunk
-        const u32x4 val = *(const u32x4*)(stg + pr * 80 + c4 * 16);
+      for (int h = 0; h < (32 * NCH) / 64; ++h) {
+        const int idx = lane + 64 * h, pr = idx / NCH, c = idx - pr * NCH;
+        const u32x4 val = *(const u32x4*)(stg + pr * SP + c * 16);
         const int col = j0 + pr;
         if (row < a.mi && col < a.mj && !(C16_ABL & 1)) {
           const int64_t pix = ((int64_t)b * a.ho + a.oy0 + a.osy * row) * a.wo + a.ox0 + a.osx * col;
-          const int n = n0 + nloc + c4 * 8;
+          const int n = n0 + wc * Geo::WCH + c * 8;
           *(u32x4*)(yg + pix * a.ldy + n) = val;
           if (y2g) *(u32x4*)(y2g + pix * a.ldy2 + n) = val;
         }

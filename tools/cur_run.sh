@@ -1,4 +1,5 @@
-bash tools/gpu.sh r05u \
- 'tA|500|env LIC_PARITY_RECORD=gpurun_out/r05u/parity_configs.jsonl python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_net.py tests/test_gpu_source_net.py -q -rx --timeout 300 --timeout-method thread -p no:cacheprovider' \
- 'tB|500|python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider --ignore=tests/test_gpu_configs.py --ignore=tests/test_gpu_net.py --ignore=tests/test_gpu_source_net.py' \
- 'smoke|200|python -u -c "import __graft_entry__ as g; g.smoke(); print(\"SMOKE OK\")"'
+bash tools/gpu.sh r05w \
+ 'c16tests|300|python -u -m pytest tests/test_gpu_conv16.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider' \
+ 'cb|150|python -u tools/conv_bench.py --dtype fp16 --auto-only --only wnsa3x3@64,rbws_conv2@128,wnsa7x7@64,conv5x5s2@128,rbneck3x3_96@64' \
+ 'cbnorot|150|env LIC_C16_ROT=0 python -u tools/conv_bench.py --dtype fp16 --auto-only --only wnsa3x3@64,rbws_conv2@128,wnsa7x7@64,conv5x5s2@128,rbneck3x3_96@64' \
+ 'bench16|300|python -u bench.py --precision fp16 --no-extras'
