@@ -167,4 +167,4 @@ def check_x6_rate_not_worse(d_bpp: dict) -> None:
         if d_bpp["fp32x6"] > max(1e-5, d_bpp["fp32"]) + 1e-12:
             import pytest
             pytest.xfail(f"fp32x6 free-running d_bpp {d_bpp['fp32x6']:.3e} > max(1e-5, exact fp32 "
-                         f"{d_bpp['fp32']:.3e}): near-tie cascade (DESIGN.md section 3)")
+                         f"{d_bpp['fp32']:.3e}): near-tie cascade (DESIGN.md sections 3 and 6)")

@@ -1,5 +1,6 @@
-bash tools/gpu.sh r05w \
+bash tools/gpu.sh r05x \
  'c16tests|300|python -u -m pytest tests/test_gpu_conv16.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider' \
- 'cb|150|python -u tools/conv_bench.py --dtype fp16 --auto-only --only wnsa3x3@64,rbws_conv2@128,wnsa7x7@64,conv5x5s2@128,rbneck3x3_96@64' \
- 'cbnorot|150|env LIC_C16_ROT=0 python -u tools/conv_bench.py --dtype fp16 --auto-only --only wnsa3x3@64,rbws_conv2@128,wnsa7x7@64,conv5x5s2@128,rbneck3x3_96@64' \
+ 'gdn|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --gdn gdn --only gdn1x1@128,gdn1x1@32' \
+ 'gdnr1|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --gdn gdn_r1 --only gdn1x1@128' \
+ 'cb1|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --only proj1x1@64,c1x1@128,qkv1x1@64,qkv1x1@16' \
  'bench16|300|python -u bench.py --precision fp16 --no-extras'
