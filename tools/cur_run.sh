@@ -1,6 +1,5 @@
-bash tools/gpu.sh r05x \
- 'c16tests|300|python -u -m pytest tests/test_gpu_conv16.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider' \
- 'gdn|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --gdn gdn --only gdn1x1@128,gdn1x1@32' \
- 'gdnr1|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --gdn gdn_r1 --only gdn1x1@128' \
- 'cb1|120|python -u tools/conv_bench.py --dtype fp16 --auto-only --only proj1x1@64,c1x1@128,qkv1x1@64,qkv1x1@16' \
- 'bench16|300|python -u bench.py --precision fp16 --no-extras'
+bash tools/gpu.sh r05y \
+ 'tA|500|env LIC_PARITY_RECORD=gpurun_out/r05y/parity_configs.jsonl python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_net.py tests/test_gpu_source_net.py -q -rx --timeout 300 --timeout-method thread -p no:cacheprovider' \
+ 'tB|500|python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider --ignore=tests/test_gpu_configs.py --ignore=tests/test_gpu_net.py --ignore=tests/test_gpu_source_net.py' \
+ 'smoke|200|python -u -c "import __graft_entry__ as g; g.smoke(); print(\"SMOKE OK\")"' \
+ 'bench|500|python -u bench.py'
