@@ -1,5 +1,5 @@
-bash tools/gpu.sh r05y \
- 'tA|500|env LIC_PARITY_RECORD=gpurun_out/r05y/parity_configs.jsonl python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_net.py tests/test_gpu_source_net.py -q -rx --timeout 300 --timeout-method thread -p no:cacheprovider' \
- 'tB|500|python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider --ignore=tests/test_gpu_configs.py --ignore=tests/test_gpu_net.py --ignore=tests/test_gpu_source_net.py' \
- 'smoke|200|python -u -c "import __graft_entry__ as g; g.smoke(); print(\"SMOKE OK\")"' \
- 'bench|500|python -u bench.py'
+T=r05z
+bash tools/gpu.sh $T \
+ "pmcF|150|timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/$T/pmcF -o run -- python3 tools/conv_bench.py --dtype fp16 --auto-only --iters 5 --only proj1x1@64,c1x1@128,wnsa3x3@16" \
+ "pmcW|150|timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/$T/pmcW -o run -- python3 tools/conv_bench.py --dtype fp16 --auto-only --iters 5 --only proj1x1@64,c1x1@128,wnsa3x3@16" \
+ "pmcS|150|timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM --output-format csv -d gpurun_out/$T/pmcS -o run -- python3 tools/conv_bench.py --dtype fp16 --auto-only --iters 5 --only proj1x1@64,wnsa3x3@16"
