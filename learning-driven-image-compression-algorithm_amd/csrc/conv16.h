@@ -577,13 +577,14 @@ int conv16_dispatch_impl(const lic_conv_args& a, hipStream_t s, int& status) {
       // 32-channel blocks (more, smaller workgroups: up to three per CU) unless that re-reads the halo of a
       // big grid too often: 3x3 192->192 @16^2 B=32 19.2 -> 17.4 us, 224->128 13.3 -> 12.3 (r05za).
       // A/B: LIC_C16S_CT=1/2/3 forces the channel tiles per workgroup
+      // a candidate that declines (LDS or alignment) falls through to the next one
       static const int force_ct = wd_env("LIC_C16S_CT", 0);
-      if ((force_ct == 1 || (force_ct == 0 && sblocks(1) <= 2048)) && a.copad % 32 == 0)
-        return try_conv16s<T, 3, 3, 1>(a, s, status);
-      if (force_ct == 2 && a.copad % 64 == 0) return try_conv16s<T, 3, 3, 2>(a, s, status);
-      if (a.copad % 96 == 0 && sblocks(3) >= 128) return try_conv16s<T, 3, 3, 3>(a, s, status);
-      if (a.copad % 64 == 0 && sblocks(2) >= 128) return try_conv16s<T, 3, 3, 2>(a, s, status);
-      if (a.copad % 32 == 0) return try_conv16s<T, 3, 3, 1>(a, s, status);
+      if ((force_ct == 1 || (force_ct == 0 && sblocks(1) <= 2048)) && a.copad % 32 == 0 &&
+          try_conv16s<T, 3, 3, 1>(a, s, status)) return 1;
+      if (force_ct == 2 && a.copad % 64 == 0 && try_conv16s<T, 3, 3, 2>(a, s, status)) return 1;
+      if (a.copad % 96 == 0 && sblocks(3) >= 128 && try_conv16s<T, 3, 3, 3>(a, s, status)) return 1;
+      if (a.copad % 64 == 0 && sblocks(2) >= 128 && try_conv16s<T, 3, 3, 2>(a, s, status)) return 1;
+      if (a.copad % 32 == 0 && try_conv16s<T, 3, 3, 1>(a, s, status)) return 1;
     }
   }
   if (a.mi < 16 || a.mj < 32) return 0;

@@ -95,8 +95,13 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
         const int iy = i * a.isy + dy0, ix = j * a.isx + dx0;
         vo = (unsigned)((((int64_t)(b * a.h + iy) * a.w + ix) * a.ldx + lh * 8) * 2);
       }
+      // a ragged channel count (ci = 8 for the tap-mode first convs): the half past ci reads zeros, not
+      // the next pixel's channels (the KT > 1 path guards the same way)
+      const bool ragged = (a.ci & 15) != 0;
 #pragma unroll
-      for (int kk = 0; kk < KST; ++kk) xf[kk] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, kk * 32, 0);
+      for (int kk = 0; kk < KST; ++kk)
+        xf[kk] = __builtin_amdgcn_raw_buffer_load_b128(
+            xrs, ragged && kk * 16 + lh * 8 >= a.ci ? 0x80000000u : vo, kk * 32, 0);
     } else {
       int b = 0, iy0 = -(1 << 20), ix0 = 0;   // past the map: every tap out of the image
       if (m < p.M && lh * 8 < a.ci) {

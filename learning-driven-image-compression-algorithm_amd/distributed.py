@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import os
 import signal
+import threading
 import socket
 import subprocess
 import sys
@@ -58,7 +59,10 @@ def launch_workers(cmd: Sequence[str], n: int, poll_s: float = 0.2) -> int:
                 p.terminate()
         raise SystemExit(128 + signum)
 
-    old = {sig: signal.signal(sig, _stop) for sig in (signal.SIGTERM, signal.SIGINT)}
+    # signal.signal works in the main thread only; from a worker thread the finally block's kill is the
+    # only clean-up
+    old = ({sig: signal.signal(sig, _stop) for sig in (signal.SIGTERM, signal.SIGINT)}
+           if threading.current_thread() is threading.main_thread() else {})
     try:
         for r in range(n):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),

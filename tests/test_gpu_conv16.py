@@ -332,7 +332,10 @@ def test_gemm16_gdn_residual(dtype):
 # ---- wba16 (csrc/wba16.hip): 16-bit qkv Linear + window attention in one launch ----
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("B,H,W,shift", [(4, 64, 64, 4), (2, 32, 48, 0), (3, 16, 24, 4)])
+# (16|32, 64, 64): 1024 / 2048 windows, more than the persistent grid's workgroups, so every workgroup walks
+# several windows (next-window prefetch, LDS reuse without a barrier, per-window mask: ADVICE r5)
+@pytest.mark.parametrize("B,H,W,shift", [(4, 64, 64, 4), (2, 32, 48, 0), (3, 16, 24, 4), (16, 64, 64, 4),
+                                         (32, 64, 64, 0)])
 def test_wba16_matches_unfused(dtype, B, H, W, shift):
     """The fused launch against the two-launch path (qkv Linear -> win_attn, whose own parity against
     the oracle is tests/test_gpu_attn.py) on the same operands: WinBasedAttention, reference
