@@ -12,9 +12,9 @@ The headline runs at fp32 grade (the reference computes in fp32, model/net_ga.py
 `--precision auto` (default) times precision='fp32x6' -- fp32 activations and accumulation, every
 conv product formed from six bf16 MFMA products of exact three-part splits (all 24 significand
 bits, fp32 exponent range, dropped terms <= 2^-26 relative; csrc/conv_split_wd.hip) -- when
-its parity leg on the TIMED batch (seed-0 weights, seed-1000 input of rank 0) meets the
-north-star bar with no more flipped symbols (oracle near-ties and their cascades) than the
-exact-fp32 path on the same batch, else exact fp32 (v_mfma_f32_32x32x2_f32).  Extra
+its parity legs (seed-0 weights, CPU oracle) meet the north-star bar on a panel of ten seeded batches (the timed one and the config-2 test batch among
+them; gate_panel) with no more flipped symbols in total (oracle near-ties and their cascades) and no
+worse a worst free-running rate than the exact-fp32 path, else exact fp32 (v_mfma_f32_32x32x2_f32).  Extra
 fields: roofline (dominant kernel: the 3x3 192->192 convolution of Win_noShift_Attention at
 64x64, timed with HIP events on its launch stream, against the matching MFMA peak),
 a_model (analysis stack, BASELINE config 2), cpu_baseline (the oracle restatement on this
@@ -231,23 +231,14 @@ def bench_input(batch, size, rank):
     return torch.rand(batch, 3, size, size, generator=g) * 2 - 1
 
 
-def parity_check(arch, precision, size, device, batch=1):
-    """The timed batch (rank 0's input, the timed net's seed-0 weights) through the HIP path and
-    the CPU oracle: bpp / PSNR deltas, the symbol flips and how many of them are near-ties of the
-    oracle's y - mu (|frac - 1/2| < TIE_EPS: fp32 summation order, tests/parity.py), and whether
-    the north-star bar holds (bpp 1e-5 against the oracle conditioned on the same symbols -- the
-    flips' measured bits reported beside it --, PSNR 1e-4 dB, flips at most 3e-5 of the symbols,
-    each a near-tie or its cascade)."""
+def _parity_metrics(net, x, ref, P, batch, size, device, label):
+    """One forward of `net` on x against the oracle run `ref`: bpp / PSNR deltas, the symbol flips and
+    how many of them are near-ties of the oracle's y - mu (|frac - 1/2| < TIE_EPS: fp32 summation
+    order, tests/parity.py), and whether the north-star bar holds on this batch (bpp 1e-5 against the
+    oracle conditioned on the same symbols -- the flips' measured bits reported beside it --, PSNR
+    1e-4 dB, flips at most 3e-5 of the symbols, each a near-tie or its cascade)."""
     from oracle import ref_cpu as R
-    net = build_net(arch, precision, size, batch, "cpu", seed=0)
-    P = {k: v.detach().float() for k, v in net.state_dict().items()}
-    net = net.to(device)
-    x = bench_input(batch, size, 0)
     bpp, v_mse, v_psnr = net(x.to(device), "test", return_intermediates=True)
-    key = (arch, size, batch)            # same seeded weights and input for every precision
-    if key not in _ORACLE_CACHE:
-        _ORACLE_CACHE[key] = R.net_forward(x, P, arch=arch)
-    ref = _ORACLE_CACHE[key]
     ne = net.last["symbols"].cpu() != ref["symbols"]
     flips = int(ne.sum())
     d = ref["z3"] - ref["means"]
@@ -280,10 +271,79 @@ def parity_check(arch, precision, size, device, batch=1):
             "d_bpp": d_bpp, "d_bpp_same_symbols": d_ctx, "flip_bits": round(flip_bits, 4),
             "psnr_db": round(v_psnr.item(), 5), "d_psnr_db": d_psnr,
             "symbol_flips": flips, "near_tie_flips": ties, "unexplained_flips": unexplained,
-            "symbol_mismatch_frac": flips / ref["symbols"].numel(),
-            "batch": f"timed batch of rank 0 (weights seed 0, input seed 1000, {batch} x {size}x{size})",
+            "symbol_mismatch_frac": flips / ref["symbols"].numel(), "batch": label,
             "meets_north_star_bar": bool(d_ctx <= bar and d_bpp <= bar + abs(flip_bits) / px and d_psnr <= 1e-4
                                          and flips / ne.numel() <= 3e-5 and unexplained == 0)}
+
+
+def _oracle(arch, size, batch, seed, P):
+    from oracle import ref_cpu as R
+    key = (arch, size, batch, seed)      # same seeded weights and input for every precision
+    if key not in _ORACLE_CACHE:
+        _ORACLE_CACHE[key] = R.net_forward(panel_input(batch, size, seed), P, arch=arch)
+    return _ORACLE_CACHE[key]
+
+
+def panel_input(batch, size, seed):
+    """Seeded uniform [-1, 1) images (seed 1000 + rank = the timed batch of that rank, bench_input; seed 22 =
+    tests/test_gpu_configs.py's config-2 batch)."""
+    return torch.rand(batch, 3, size, size, generator=torch.Generator(device="cpu").manual_seed(seed)) * 2 - 1
+
+
+def parity_check(arch, precision, size, device, batch=1):
+    """The timed batch (rank 0's input, the timed net's seed-0 weights) through the HIP path and the
+    CPU oracle (_parity_metrics)."""
+    net = build_net(arch, precision, size, batch, "cpu", seed=0)
+    P = {k: v.detach().float() for k, v in net.state_dict().items()}
+    net = net.to(device)
+    ref = _oracle(arch, size, batch, 1000, P)
+    return _parity_metrics(net, bench_input(batch, size, 0), ref, P, batch, size, device,
+                           f"timed batch of rank 0 (weights seed 0, input seed 1000, {batch} x {size}x{size})")
+
+
+# the gate's panel of input seeds: the timed batch of rank 0 (1000), the config-2 test batch
+# (tests/test_gpu_configs.py, 22) and eight more -- the committed panel profiles/r06/parity_panel_cfg2.jsonl
+GATE_SEEDS = (1000, 22, 1, 2, 3, 4, 5, 6, 7, 8)
+
+
+def gate_panel(arch, size, device, batch, seeds=GATE_SEEDS):
+    """The precision gate's evidence: fp32x6 and exact fp32 on every panel batch against the oracle.
+    fp32x6 is the headline when (1) on EVERY batch each of its flips is an oracle near-tie or its cascade,
+    its rate on the same symbols is within 1e-5 bpp and its PSNR within 1e-4 dB, (2) it flips no more
+    symbols over the panel than exact fp32 and (3) its worst free-running delta-bpp is no worse than
+    max(1e-5, exact fp32's worst).  Whether a near-tie flips (the oracle's own y - mu is ~6e-7 relative
+    from the exact value, profiles/r06/attribution_cfg2_seed22.json) is a coin toss per batch for ANY fp32
+    summation order, so the decision is on the panel, not on one batch (VERDICT r5 next #1)."""
+    nets, rows = {}, {"fp32x6": [], "fp32": []}
+    P = None
+    for prec in rows:
+        n = build_net(arch, prec, size, batch, "cpu", seed=0)
+        if P is None:
+            P = {k: v.detach().float() for k, v in n.state_dict().items()}
+        nets[prec] = n.to(device)
+    for i, seed in enumerate(seeds):
+        print(f"gate panel: batch {i + 1}/{len(seeds)} (input seed {seed})", file=sys.stderr, flush=True)
+        ref = _oracle(arch, size, batch, seed, P)
+        x = panel_input(batch, size, seed)
+        for prec, n in nets.items():
+            r = _parity_metrics(n, x, ref, P, batch, size, device,
+                                f"weights seed 0, input seed {seed}, {batch} x {size}x{size}")
+            r["seed"] = seed
+            rows[prec].append(r)
+    del nets
+    torch.cuda.empty_cache()
+    tot = {p: sum(r["symbol_flips"] for r in rs) for p, rs in rows.items()}
+    worst = {p: max(r["d_bpp"] for r in rs) for p, rs in rows.items()}
+    per_batch_ok = all(r["unexplained_flips"] == 0 and r["d_psnr_db"] <= 1e-4 and
+                       r["d_bpp_same_symbols"] <= 1e-5 * max(1.0, abs(r["bpp_ref"])) for r in rows["fp32x6"])
+    ok = per_batch_ok and tot["fp32x6"] <= tot["fp32"] and worst["fp32x6"] <= max(1e-5, worst["fp32"])
+    brief = lambda r: {k: r[k] for k in ("seed", "symbol_flips", "near_tie_flips", "unexplained_flips", "d_bpp",
+                                         "d_bpp_same_symbols", "d_psnr_db", "meets_north_star_bar")}
+    return ok, {"seeds": list(seeds), "total_flips": tot, "worst_d_bpp": worst,
+                "batches_meeting_bar": {p: sum(r["meets_north_star_bar"] for r in rs) for p, rs in rows.items()},
+                "fp32x6_every_batch_ties_and_same_symbol_rate_ok": per_batch_ok,
+                "rows": {p: [brief(r) for r in rs] for p, rs in rows.items()}}, \
+        rows["fp32x6"][0], rows["fp32"][0]
 
 
 def forward_rate(net, x, iters=10):
@@ -361,6 +421,9 @@ def main():
                          "batch meets the north-star bar with no more flipped symbols than exact fp32 on that batch "
                          "(checked first, on rank 0), else exact fp32; fp32x3 (fp16 parts, narrower than fp32) and "
                          "fp16 activations are extras")
+    ap.add_argument("--gate-seeds", default=",".join(str(v) for v in GATE_SEEDS),
+                    help="input seeds of the precision gate's panel (1000 = the timed batch, 22 = the config-2 test "
+                         "batch)")
     ap.add_argument("--no-extras", action="store_true", help="skip cpu baseline / parity / fp16 legs")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--post-processing", action="store_true", help="HAN post-processing head (eval_net flag)")
@@ -392,14 +455,13 @@ def main():
         return
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    gate = gate32 = None
+    gate = gate32 = panel = None
     if args.precision == "auto":
         ok = 0.0
         if rank == 0:
-            gate = parity_check(args.arch, "fp32x6", args.size, device, args.batch)
-            gate32 = parity_check(args.arch, "fp32", args.size, device, args.batch)
-            ok = 1.0 if (gate["meets_north_star_bar"] and
-                         gate["symbol_flips"] <= gate32["symbol_flips"]) else 0.0
+            seeds = tuple(int(v) for v in args.gate_seeds.split(","))
+            okp, panel, gate, gate32 = gate_panel(args.arch, args.size, device, args.batch, seeds)
+            ok = 1.0 if okp else 0.0
         ok = D.max_over_ranks(ok, world, device)
         args.precision = "fp32x6" if ok > 0 else "fp32"
         torch.cuda.empty_cache()
@@ -502,13 +564,14 @@ def main():
                 result[other] = extra_leg(args, other, x, device, gf_a)
         if gate is not None:
             result["precision_gate"] = {
-                "rule": "headline = fp32x6 (fp32 grade) when its parity leg on the timed batch (rank 0's input, "
-                        "the timed seed-0 weights, CPU oracle) meets the north-star bar (bpp 1e-5, PSNR 1e-4 dB, "
-                        "every symbol flip an oracle near-tie |frac(y-mu)-1/2| < 2e-4 or its cascade) with no more "
-                        "flips than the exact-fp32 path on the same batch, else exact fp32.  0 flips is not "
-                        "attainable by any fp32 summation order other than the oracle's own on this batch: the "
-                        "exact-fp32 path flips its near-ties too (exact_fp32_parity)",
-                "fp32x6_parity": gate, "exact_fp32_parity": gate32, "chosen": args.precision}
+                "rule": "headline = fp32x6 (fp32 grade) when, over a panel of batches (the timed batch, input seed "
+                        "1000; the config-2 test batch, seed 22; eight more), every fp32x6 symbol flip is an oracle "
+                        "near-tie |frac(y-mu)-1/2| < 2e-4 or its cascade, its rate on the same symbols is within "
+                        "1e-5 bpp and its PSNR within 1e-4 dB on every batch, it flips no more symbols in total than "
+                        "the exact-fp32 path and its worst free-running delta-bpp is no worse than max(1e-5, exact "
+                        "fp32's worst); else exact fp32.  A near-tie within ~1e-6 of .5 flips by chance for any "
+                        "fp32 summation order, the oracle's included (profiles/r06/attribution_cfg2_seed22.json)",
+                "panel": panel, "fp32x6_parity": gate, "exact_fp32_parity": gate32, "chosen": args.precision}
         print(json.dumps(result), flush=True)
     D.finish(world)
 

@@ -91,7 +91,11 @@ typedef struct lic_conv_args {
    *     relative); wgt_split = the weights as bf16 [copad][ntaps][cpad/16][w0 16 | w1 16 | w2 16];
    * 1 = "fp32x3": fp16 parts, x_hi*W1 + x_hi*W2 + x_lo*W1 (x_lo = fp16(x - fp16(x)), ~3e-7
    *     relative per product); wgt_split = fp16 [copad][ntaps][cpad/16][W1 16 | W2 16],
-   *     W1 = fp16(w)*2^11, W2 = fp16((w - fp16(w))*2^11). */
+   *     W1 = fp16(w)*2^11, W2 = fp16((w - fp16(w))*2^11).
+   * LIC_F16 / LIC_BF16 (mfma_mode 0): wgt_split is optional -- the same 16-bit weights as wgt in
+   * MFMA-fragment order [copad/32][cpad/16][ntaps][64 lanes][8], lane = 32 * (channel half) +
+   * (row % 32), one contiguous 1 KB per A fragment (the conv16 / conv16s kernels read it when given,
+   * round 6); NULL = wgt only. */
   int32_t mfma_mode;
   const void* wgt_split;
 } lic_conv_args;
@@ -197,6 +201,11 @@ int lic_nchw_to_nhwc(int32_t dtype, const float* x, int32_t n, int32_t c, int32_
  * (channels 3.. zero) so the 3->192 convolutions can run on MFMA. */
 int lic_rb3_fwd(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t ldx,
                 const float* params, void* y, int32_t ldy, lic_stream_t stream);
+/* nblk (1..3) consecutive ResidualBottleneck(3) blocks in one launch (the a_model's first three,
+ * net_ga.py:262-264): params = nblk x the 20 floats above; equals nblk lic_rb3_fwd launches (the
+ * intermediate blocks rounded to dtype where those launches store them).  y must not alias x. */
+int lic_rb3_chain_fwd(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t ldx,
+                      const float* params, int32_t nblk, void* y, int32_t ldy, lic_stream_t stream);
 int lic_nhwc_to_nchw(int32_t dtype, const void* x, int32_t n, int32_t h, int32_t w, int32_t c,
                      int32_t ldx, float* y, lic_stream_t stream);
 /* y = a + b (views, same geometry). */

@@ -52,7 +52,7 @@ EXPORTED_SYMBOLS = (
     "lic_rate_train_parts", "lic_rate_train_fwd", "lic_rate_train_bwd", "lic_recon_train_blocks",
     "lic_recon_train_fwd", "lic_recon_train_bwd", "lic_dwconv_wgrad_workspace", "lic_dwconv_wgrad",
     "lic_resunit_fwd", "lic_patches", "lic_wba_qkv_attn_fwd", "lic_wba16_qkv_attn_fwd", "lic_pack_taps",
-    "lic_pack_taps_batch", "lic_pack_block_elems",
+    "lic_pack_taps_batch", "lic_pack_block_elems", "lic_rb3_chain_fwd",
 )
 LIC_EB_PARAMS = 58
 
@@ -226,6 +226,7 @@ def load():
         "lic_psnr_finalize": [V, I, I, D, V, V, V],
         "lic_nchw_to_nhwc": [I, V, I, I, I, I, V, I, I, V],
         "lic_rb3_fwd": [I, V, I, I, I, I, V, V, I, V],
+        "lic_rb3_chain_fwd": [I, V, I, I, I, I, V, I, V, I, V],
         "lic_nhwc_to_nchw": [I, V, I, I, I, I, I, V, V],
         "lic_add": [I, V, I, V, I, I, I, V, I, V],
         "lic_copy": [I, V, I, I, I, I, V, I, V],

@@ -119,7 +119,37 @@ struct C16Plan {
   unsigned wrec;      // bytes of the packed weights
   int nst;            // stages = nchunks * ngroups
   int fast_epi;       // the register epilogue variant (c16_fast_epi): 0 none, 1 plain / + r1, 2 gate
+  int frag;           // 1: the weights come from a.wgt_split in MFMA-fragment order (c16_frag_ok)
+  // byte strides of the weight source (either layout, c16_wstrides): 32-row block, 16-channel chunk, tap;
+  // and per lane: row, 16-B channel half
+  int ws_co, ws_k, ws_tap, wl_row, wl_half;
 };
+
+// 16-bit weights in MFMA-fragment order (lic_conv_args.wgt_split for LIC_F16 / LIC_BF16, include/lic.h):
+// [copad/32][cpad/16][ntaps][64 lanes][16 B], lane = 32 * (channel half) + (row % 32) -- one fragment is
+// one contiguous 1 KB (8 cache lines) instead of 32 rows x 32 B on 32 lines
+inline bool c16_frag_ok(const lic_conv_args& a) {
+  return a.wgt_split != nullptr && a.mfma_mode == 0 && (a.dtype == LIC_F16 || a.dtype == LIC_BF16) &&
+         ((uintptr_t)a.wgt_split % 16) == 0 && a.copad % 32 == 0 && a.cpad % 16 == 0 && wd_env("LIC_W16_FRAG", 1);
+}
+// the weight source strides of both layouts: [copad][ntaps][cpad] rows, or fragment order
+template <typename Plan>
+inline void c16_wstrides(const lic_conv_args& a, Plan& p) {
+  const int nch = a.cpad / 16;
+  if (p.frag) {
+    p.ws_co = nch * a.ntaps * 1024;
+    p.ws_k = a.ntaps * 1024;
+    p.ws_tap = 1024;
+    p.wl_row = 16;
+    p.wl_half = 512;
+  } else {
+    p.ws_co = 32 * a.ntaps * a.cpad * 2;
+    p.ws_k = 32;
+    p.ws_tap = a.cpad * 2;
+    p.wl_row = a.ntaps * a.cpad * 2;
+    p.wl_half = 16;
+  }
+}
 
 // S = 1: stages are (chunk, group of G taps = G/KW tap rows).  S = 2: stages are (chunk, input-parity
 // phase (py, px)): phase taps (2a+py, 2b+px) form a stride-1 grid of ceil((KH-py)/2) x ceil((KW-px)/2)
@@ -195,7 +225,8 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
   }
 
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)p.xrec, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, (short)0, (int)p.wrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.frag ? a.wgt_split : a.wgt), (short)0, (int)p.wrec, 0x00020000);
 
   // ---- per-lane source offsets of this wave's pieces (fixed for the launch) ----
   // halo piece P = wave + NW*m: slot q = 64P + lane -> halo pixel q>>1, stored half q&1 holds
@@ -219,9 +250,7 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
   // weight piece Q (rotated by 4 waves to balance the per-wave piece counts): tap Q / (BN/32),
   // channels (Q % (BN/32))*32 + lane/2, stored half lane&1 holds channel half (lane&1) ^ bit3(n)
   const int wq0 = (wave + 4) % NW;
-  const unsigned woff_lane =
-      (unsigned)(((lane >> 1) * a.ntaps * a.cpad + (((lane & 1) ^ ((lane >> 4) & 1)) * 8)) * 2);
-  const int wrow_bytes = a.ntaps * a.cpad * 2;   // one output channel's packed weights
+  const unsigned woff_lane = (unsigned)((lane >> 1) * p.wl_row + ((lane & 1) ^ ((lane >> 4) & 1)) * p.wl_half);
 
   // (a chunk order rotated per workgroup, so that the workgroups sharing an L2 stream different weight
   // lines, measured 0.3-2 % slower: r05w)
@@ -246,7 +275,7 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
         const int ta = tt / kwp, tb = tt - ta * kwp;
         tap = (2 * ta + py) * KW + 2 * tb + px;
       }
-      const int soff = (n0 + nq * 32) * wrow_bytes + tap * a.cpad * 2 + k * 32;
+      const int soff = ((n0 >> 5) + nq) * p.ws_co + tap * p.ws_tap + k * p.ws_k;
       c16_dma(wrs, smem + 2 * HBYTES + wb * WBYTES + Q * 1024, woff_lane, soff);
     }
   };
@@ -528,6 +557,8 @@ int try_conv16(const lic_conv_args& a, hipStream_t s, int& status) {
   p.wrec = (unsigned)wbytes;
   p.nst = p.nchunks * Geo::NG;
   p.fast_epi = wd_env("LIC_C16_FAST_EPI", 1) ? c16_fast_epi(a, 2, BN == 96) : 0;
+  p.frag = c16_frag_ok(a) ? 1 : 0;
+  c16_wstrides(a, p);
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   dim3 grid((unsigned)blocks, a.copad / BN);
   auto kern = p.fast_epi == 1 ? conv16_kernel<T, KH, KW, S, G, BN, WN, 1> : conv16_kernel<T, KH, KW, S, G, BN, WN, 0>;

@@ -30,6 +30,8 @@ struct C16sPlan {
   int npieces;        // 1-KB LDS-DMA pieces of the halo (every chunk plane)
   int main_bytes;     // LDS before bias + destination pixels: max(halo, partial tiles)
   unsigned xrec, wrec;
+  int frag;           // weights from a.wgt_split in MFMA-fragment order (conv16.h c16_frag_ok)
+  int ws_co, ws_k, ws_tap, wl_row, wl_half;   // weight source strides (conv16.h c16_wstrides)
 };
 
 template <typename T, int MASK>
@@ -112,7 +114,8 @@ __global__ __launch_bounds__(256, 1) void conv16s_kernel(const lic_conv_args a, 
   }
 
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)p.xrec, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, (short)0, (int)p.wrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.frag ? a.wgt_split : a.wgt), (short)0, (int)p.wrec, 0x00020000);
 
   // ---- the whole halo by LDS-DMA: 16-B slot q = chunk q / (2 HPIX), halo pixel (q / 2) % HPIX, stored
   // half q & 1 = channel half (q & 1) ^ bit3(column) ----
@@ -130,8 +133,7 @@ __global__ __launch_bounds__(256, 1) void conv16s_kernel(const lic_conv_args a, 
 
   // ---- weights: A fragment (tap t, chunk kc, channel tile i) = rows n0 + 32 i + l32, channels
   // 16 kc + 8 lh .. +7 (16 B): per-lane offset + scalar offset ----
-  const int cpad2 = a.cpad * 2;
-  const unsigned wl = (unsigned)((l32 * NTAPS * a.cpad + 8 * lh) * 2);
+  const unsigned wl = (unsigned)(l32 * p.wl_row + lh * p.wl_half);
   const int nchunks = p.nchunks;
   const int ncw = (nchunks - wave + NW - 1) / NW;   // this wave's chunks: wave, wave + NW, ...
   // the chunk order is rotated by the workgroup (a bijection of the chunks): the workgroups sharing an
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(256, 1) void conv16s_kernel(const lic_conv_args a, 
     const int kc = chunk_of(cidx);
 #pragma unroll
     for (int i = 0; i < CT; ++i)
-      f[i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wl, ((n0 + 32 * i) * NTAPS + t) * cpad2 + kc * 32, 0);
+      f[i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, wl, ((n0 >> 5) + i) * p.ws_co + t * p.ws_tap + kc * p.ws_k, 0);
   };
 
   // ---- B fragments: pixel l32 of fragment j = tile row 2j + (l32 >> 4), column l32 & 15 ----
@@ -249,6 +251,8 @@ int try_conv16s(const lic_conv_args& a, hipStream_t s, int& status) {
   if (smem > 160 * 1024) return 0;
   p.xrec = (unsigned)xbytes;
   p.wrec = (unsigned)wbytes;
+  p.frag = c16_frag_ok(a) ? 1 : 0;
+  c16_wstrides(a, p);
   const int64_t blocks = (int64_t)a.n * p.tiles_y * p.tiles_x;
   dim3 grid((unsigned)blocks, a.copad / Geo::BN);
   auto kern = conv16s_kernel<T, KH, KW, CT>;

@@ -468,6 +468,29 @@ def split_weights(pk: ConvPack, mode: int = 1) -> Optional[torch.Tensor]:
     return out
 
 
+_FRAG16 = os.environ.get("LIC_W16_FRAG", "1") != "0"
+
+
+def frag16_weights(pk: ConvPack) -> Optional[torch.Tensor]:
+    """A 16-bit pack's weights in MFMA-fragment order ([copad/32][cpad/16][ntaps][64][8]: one contiguous
+    1 KB per A fragment; include/lic.h wgt_split), which the conv16 / conv16s kernels read instead of the
+    [copad][ntaps][cpad] rows (32 cache lines per fragment).  Built on a pack's SECOND use with the same
+    weights and never inside a hipGraph capture, so the training step -- its packs change every step --
+    never pays for the copy and a capture never records it; cached on the pack."""
+    w = pk.w
+    if not _FRAG16 or w.dtype == torch.float32 or w.shape[0] % 32 or w.shape[2] % 16 or not w.is_cuda:
+        return None
+    ent = pk.__dict__.get("_frag16")
+    if ent is not None and ent[0] is w and ent[1] == w._version:
+        if ent[2] is not None or ent[3] < 1 or torch.cuda.is_current_stream_capturing():
+            return ent[2]
+        out = _frag_order([w]).contiguous()
+        pk.__dict__["_frag16"] = (w, w._version, out, ent[3] + 1)
+        return out
+    pk.__dict__["_frag16"] = (w, w._version, None, 1)
+    return None
+
+
 def stride2_phase_packs(pk: ConvPack) -> Optional[List[ConvPack]]:
     """The input-parity phases of a stride-2 k x k ConvPack (k >= 3, more than 16 input channels):
     four sub-packs holding the taps whose row / column offsets share one parity (5x5: 9, 6, 6 and
@@ -603,6 +626,10 @@ def conv(x: Act, pk: ConvPack, out: Optional[Act] = None, *, act: int = _ffi.ACT
     a.out_shuffle = mode
     a.force_direct = 1 if force_direct else 0
     a.force_mfma_generic = 1 if force_generic else 0
+    if x.dtype != torch.float32 and pk.groups == 1:
+        wf = frag16_weights(pk)
+        if wf is not None:
+            a.wgt_split = _dp(wf)
     smode = split_mode()
     if smode == 1 and prologue == _ffi.PRO_SQUARE:
         smode = 2   # fp32x3's fp16 parts: x^2 leaves fp16's range from |x| >= 256 (GDN) -> bf16 parts
@@ -821,6 +848,21 @@ def rb3(x: Act, params: torch.Tensor, out: Optional[Act] = None) -> Act:
         out = Act(torch.empty((x.B, x.H, x.W, epc), dtype=x.dtype, device=x.t.device), 0, 3, epc)
     check(_lib().lic_rb3_fwd(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.ld, _dp(params), out.ptr, out.ld,
                              stream_handle()))
+    return out
+
+
+def rb3_chain(x: Act, params: torch.Tensor, nblk: int, out: Optional[Act] = None) -> Act:
+    """nblk consecutive fused ResidualBottleneck(3) blocks in one launch (params: nblk x 20 fp32);
+    equals nblk rb3() calls.  The output pixels are zero-padded to 16 bytes (Act.zpad)."""
+    if x.c != 3:
+        raise ValueError("rb3_chain expects a 3-channel view")
+    if params.numel() != 20 * nblk or params.dtype != torch.float32 or not params.is_contiguous():
+        raise ValueError("rb3_chain: params must be nblk x 20 contiguous fp32")
+    if out is None:
+        epc = 16 // x.t.element_size()
+        out = Act(torch.empty((x.B, x.H, x.W, epc), dtype=x.dtype, device=x.t.device), 0, 3, epc)
+    check(_lib().lic_rb3_chain_fwd(dtype_id(x.dtype), x.ptr, x.B, x.H, x.W, x.ld, _dp(params), nblk, out.ptr,
+                                   out.ld, stream_handle()))
     return out
 
 

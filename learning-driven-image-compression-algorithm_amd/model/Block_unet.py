@@ -72,8 +72,11 @@ class ResidualBottleneck(nn.Module):
                                     Conv2d(N // 2, N // 2, kernel_size=3, stride=1, padding=1), act(),
                                     conv1x1(N // 2, N))
 
+    def rb3_ok(self, x: Act) -> bool:
+        return x.c == 3 and self.branch[0].out_channels == 1
+
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
-        if x.c == 3 and self.branch[0].out_channels == 1 and out is None:
+        if self.rb3_ok(x) and out is None:
             return Fn.rb3(x, self._rb3_params())                 # whole block in one pass
         t = self.branch[0].run(x, act=ACT_GELU)
         t = self.branch[2].run(t, act=ACT_GELU)

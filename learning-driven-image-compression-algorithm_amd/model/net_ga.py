@@ -172,8 +172,11 @@ class analysisTransformModel(nn.Module):
 
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
         t = self.transform
-        for i in range(3):
-            x = t[i].run(x)
+        if all(t[i].rb3_ok(x) for i in range(3)) and os.environ.get("LIC_RB3_CHAIN", "1") != "0":
+            x = Fn.rb3_chain(x, self._rb3_chain_params(), 3)   # the three blocks in one launch
+        else:
+            for i in range(3):
+                x = t[i].run(x)
         x = t[3].run(x)
         x = t[4].run(x)
         x = t[6].run(x, pad=(1, 1, 2, 2))     # ZeroPad2d((1, 2, 1, 2)) = left 1, right 2, top 1, bottom 2
@@ -185,6 +188,15 @@ class analysisTransformModel(nn.Module):
         x = t[13].run(x)
         x = t[15].run(x, pad=(1, 1, 2, 2))
         return t[16].run(x, out)
+
+    def _rb3_chain_params(self):
+        blocks = [self.transform[i] for i in range(3)]
+        key = tuple((p.data_ptr(), p._version) for m in blocks for p in m.parameters())
+        c = self.__dict__.get("_rb3_chain_cache")
+        if c is None or c[0] != key:
+            c = (key, torch.cat([m._rb3_params() for m in blocks]).contiguous())
+            self.__dict__["_rb3_chain_cache"] = c
+        return c[1]
 
     def forward(self, inputs):
         return self.run(Act.from_nchw(inputs)).nchw()

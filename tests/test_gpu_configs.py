@@ -21,7 +21,7 @@ import pytest
 import torch
 
 from oracle import ref_cpu as R
-from parity import (check_decoder, check_flip_sets_match, check_rate, check_symbols, check_x6_rate_not_worse,
+from parity import (check_decoder, check_flip_sets_match, check_rate, check_symbols, note_x6_vs_fp32,
                     near_tie_count, record)
 
 pytestmark = pytest.mark.gpu
@@ -99,7 +99,7 @@ def _compare_forward(arch, B, S, seed, xseed, precisions=("fp32", "fp32x6")):
     if "fp32" in masks and "fp32x6" in masks:
         n = check_flip_sets_match(masks["fp32x6"], masks["fp32"], ref)
         print(f"flip-set difference fp32x6 vs exact fp32: {n}")
-    check_x6_rate_not_worse({p: r[1] for p, r in res.items()})   # last: may end the test as an xfail
+    note_x6_vs_fp32({p: r[1] for p, r in res.items()})
 
 
 def test_cfg2_forward_b32_fp32_bit_exact_symbols():
@@ -108,3 +108,21 @@ def test_cfg2_forward_b32_fp32_bit_exact_symbols():
 
 def test_cfg3_net_unet_ha_hs_b16_512_fp32():
     _compare_forward("net_unet_ha_hs", 16, 512, 0, 23)
+
+
+@pytest.mark.timeout(900)
+def test_cfg2_gate_panel():
+    """The headline precision's parity over a panel of config-2 batches (net_ga, B=32, 256^2, seed-0 weights;
+    input seeds 1000 = the bench's timed batch, 22 = the batch above, 1..8), bench.py's precision gate run as a
+    test: on every batch each fp32x6 flip is an oracle near-tie or its cascade, the same-symbol rate is within
+    1e-5 bpp and the PSNR within 1e-4 dB; over the panel fp32x6 flips no more symbols than exact fp32 and its
+    worst free-running delta-bpp is no worse than max(1e-5, exact fp32's) (the committed
+    panel: profiles/r06/parity_panel_cfg2.jsonl)."""
+    import bench
+    ok, panel, _, _ = bench.gate_panel("net_ga", 256, torch.device(DEV), 32)
+    print(f"\n[cfg2 panel] total flips {panel['total_flips']} worst d_bpp {panel['worst_d_bpp']} "
+          f"batches meeting the bar {panel['batches_meeting_bar']}")
+    record("net_ga B=32 256x256 panel", "fp32x6 vs fp32", total_flips=panel["total_flips"],
+           worst_d_bpp=panel["worst_d_bpp"], seeds=panel["seeds"])
+    assert panel["fp32x6_every_batch_ties_and_same_symbol_rate_ok"], panel["rows"]["fp32x6"]
+    assert ok, panel

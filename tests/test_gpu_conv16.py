@@ -390,3 +390,30 @@ def test_conv16_stride2_3x3(dtype, B, H, W):
     out = m.to(DEV).run(_act(x, dtype), act=L.ACT_LRELU).nchw()
     ref = F.leaky_relu(F.conv2d(_rounded(x, dtype), _rounded(m.weight.detach().cpu(), dtype), m.bias.detach().cpu(), 2, 1))
     _check(out, ref, dtype, f"conv3x3 s2 {dtype} B={B} {H}x{W}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,stride,B,H,W", [
+    (192, 192, 3, 1, 32, 64, 64),      # conv16 3x3, 192-channel blocks
+    (96, 96, 3, 1, 32, 64, 64),        # conv16 96-channel blocks
+    (192, 192, 5, 2, 32, 128, 128),    # conv16 ZeroPad + 5x5 s2 phases
+    (192, 192, 7, 1, 32, 64, 64),      # conv16 7x7
+    (192, 192, 3, 1, 32, 16, 16),      # conv16s 3x3 @16^2
+    (224, 128, 3, 1, 32, 16, 16),      # conv16s (slice-loop cc conv)
+    (192, 192, 7, 1, 32, 16, 16),      # conv16s 7x7
+])
+def test_frag16_weights_bit_identical(dtype, cin, cout, k, stride, B, H, W):
+    """conv16 / conv16s with the weights in MFMA-fragment order (functional.frag16_weights, built on a pack's
+    second use; include/lic.h wgt_split) give the same bits as the [copad][ntaps][cpad] rows: only the load
+    addresses differ."""
+    from lic_amd.layers import Conv2d
+    import lic_amd.functional as Fn
+    torch.manual_seed(70 + k + H)
+    m = Conv2d(cin, cout, k, stride, k // 2 if stride == 1 else 0).to(DEV)
+    x = _act(torch.randn(B, cin, H, W) * 0.5, dtype)
+    pad = None if stride == 1 else (1, 1, 2, 2)
+    y_rows = m.run(x, pad=pad).t.clone()
+    pk = m.packed(x.dtype, pad if pad is not None else (m.padding[0],) * 4)
+    assert Fn.frag16_weights(pk) is not None        # second use: the fragment-order copy exists now
+    y_frag = m.run(x, pad=pad).t
+    assert torch.equal(y_rows, y_frag)

@@ -44,6 +44,38 @@ def test_rb3_fused_matches_oracle(dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("B,H,W", [(2, 33, 40), (3, 64, 96), (32, 256, 256)])
+def test_rb3_chain_equals_three_launches(dtype, B, H, W):
+    """The a_model's three ResidualBottleneck(3) blocks (net_ga.py:262-264) in one launch (lic_rb3_chain_fwd)
+    equal the three one-block launches bitwise (ragged 32 x 32 tiles included) and the oracle within the
+    dtype's bar; the output pixels are zero-padded to 16 bytes."""
+    from lic_amd.model.Block_unet import ResidualBottleneck
+    from lic_amd.functional import Act
+    import lic_amd.functional as Fn
+    torch.manual_seed(23 + H)
+    ms = [ResidualBottleneck(3) for _ in range(3)]
+    for m in ms:
+        with torch.no_grad():
+            for p in m.parameters():
+                p.normal_(0, 0.5)
+    ms = [m.to(DEV) for m in ms]
+    x = torch.rand(B, 3, H, W) * 2 - 1
+    xa = Act.from_nchw(x.to(DEV), dtype, pad16=True)
+    ref3 = xa
+    for m in ms:
+        ref3 = m.run(ref3)
+    params = torch.cat([m._rb3_params() for m in ms]).contiguous()
+    y = Fn.rb3_chain(xa, params, 3)
+    assert torch.equal(y.t, ref3.t)
+    assert y.t[..., 3:].abs().max().item() == 0.0
+    if B * H * W <= 20000:
+        r = x
+        for i, m in enumerate(ms):
+            r = R.residual_bottleneck(r, _P(m, "r"), "r")
+        _close(y.nchw(), r, dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 def test_rbws_from_padded_image(dtype):
     """ResidualBlockWithStride(3 -> 192) on the zero-padded 3-channel image runs as Cin=16 B MFMA."""
     from lic_amd.layers import ResidualBlockWithStride

@@ -1,6 +1,7 @@
 #!/bin/bash
 # tools/build_variant.sh NAME "DEFINES" file.hip... : liblic with some objects rebuilt with
-# extra defines -> tools/native/liblic_NAME.so (diagnostic A/B builds; select with LIC_LIB=)
+# extra defines -> tools/native/liblic_NAME.so (diagnostic A/B builds; select with LIC_LIB=; OUT=dir: elsewhere --
+# tools/native/*.so does not travel to the GPU box)
 set -e
 name=$1; defs=$2; shift 2
 C=learning-driven-image-compression-algorithm_amd/csrc
@@ -15,4 +16,5 @@ for o in $C/build/*.o; do
     objs="$objs $out/$b.o"
   else objs="$objs $o"; fi
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o tools/native/liblic_$name.so
+dest=${OUT:-tools/native}; mkdir -p $dest
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o $dest/liblic_$name.so
