@@ -321,6 +321,216 @@ __global__ __launch_bounds__(512, 1) void gemm16_kernel(const lic_conv_args a, c
   }
 }
 
+
+// "Wide" gemm16 (round 6): each wave owns a 32-pixel tile x all 192 channels of its block (6 accumulator
+// tiles) instead of two waves sharing every pixel tile with 96 channels each, so the CU runs 8 independent
+// pixel streams (not 4, each loaded twice), and the next tile's K step kk is issued as soon as this tile's
+// MFMAs of step kk have read it -- a whole K loop (72 MFMAs) ahead of its use instead of one epilogue.
+// The HBM-bound 1x1s were latency-bound at one tile in flight per stream (3.9 TB/s).  The
+// epilogue operands (r1 loads, or GDN's g from the fragments) are fetched before the first next-tile load
+// (loads retire in order).  Register epilogue only (plain / + r1 / GDN with g = x); same arithmetic per
+// output element as gemm16_kernel (the same MFMA sequence over the K steps): bit-identical.
+template <typename T, int KST, int PRO, int FAST>
+__global__ __launch_bounds__(512, 1) void gemm16w_kernel(const lic_conv_args a, const G16Plan p) {
+  constexpr int NW = 8, BN = 192, TN = 6;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  float* sbias = (float*)(smem + KST * BN * 32);
+  char* slots = (char*)(sbias + BN);
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int nb = blockIdx.x % p.nblk;
+  const int rank = blockIdx.x / p.nblk;
+  const int n0 = nb * BN;
+  {
+    const __amdgpu_buffer_rsrc_t wrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, (short)0, (int)p.wrec, 0x00020000);
+    const int wrow = a.ntaps * a.cpad;
+    const unsigned woff_lane = (unsigned)(((lane >> 1) * wrow + (((lane & 1) ^ ((lane >> 4) & 1)) * 8)) * 2);
+    constexpr int NPIECE = KST * BN / 32;
+    for (int P = wave; P < NPIECE; P += NW) {
+      const int kk = P / (BN / 32), nq = P - kk * (BN / 32);
+      c16_dma(wrs, smem + P * 1024, woff_lane, ((n0 + nq * 32) * wrow + kk * 16) * 2);
+    }
+    for (int n = tid; n < BN; n += NW * 64) sbias[n] = (a.bias && n0 + n < a.co) ? a.bias[n0 + n] : 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)p.xrec, 0x00020000);
+  const int mij = a.mi * a.mj;
+  const int dy0 = a.dy[0], dx0 = a.dx[0];
+  const int wlane = l32 * 32 + ((lh ^ ((l32 >> 3) & 1)) << 4);
+  char* stg = slots + wave * G16_SLOT;
+  auto voff = [&](int t) __attribute__((always_inline)) -> unsigned {
+    const int m = t * 32 + l32;
+    unsigned vo = 0x80000000u;   // past the map: out-of-range offsets read zeros
+    if (m < p.M) {
+      const int b = m / mij, rem = m - b * mij;
+      const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
+      vo = (unsigned)((((int64_t)(b * a.h + i * a.isy + dy0) * a.w + j * a.isx + dx0) * a.ldx + lh * 8) * 2);
+    }
+    return vo;
+  };
+  auto square = [&](u32x4 v) __attribute__((always_inline)) -> u32x4 {
+    if constexpr (std::is_same<T, half_t>::value) {
+      typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+      h8 hv = __builtin_bit_cast(h8, v);
+      hv = hv * hv;
+      v = __builtin_bit_cast(u32x4, hv);
+    } else {
+      T* e = (T*)&v;
+#pragma unroll
+      for (int z = 0; z < 8; ++z) {
+        const float f = to_f(e[z]);
+        e[z] = from_f<T>(f * f);
+      }
+    }
+    return v;
+  };
+
+  const int stride = p.wgs * NW;
+  int t = __builtin_amdgcn_readfirstlane(rank * NW + wave);
+  u32x4 xc[KST];
+  if (t < p.ntiles) {
+    const unsigned vo = voff(t);
+#pragma unroll
+    for (int kk = 0; kk < KST; ++kk) xc[kk] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, kk * 32, 0);
+  }
+  const T* __restrict__ r1g = (const T*)a.r1;
+  T* __restrict__ yg = (T*)a.y;
+  T* __restrict__ y2g = (T*)a.y2;
+  while (t < p.ntiles) {
+    const int tn = __builtin_amdgcn_readfirstlane(t + stride);
+    const int m = t * 32 + l32;
+    const bool pok = m < p.M;
+    int64_t pix = 0;
+    if (pok) {
+      const int b = m / mij, rem = m - b * mij;
+      const int i = rem / a.mj, j = rem - (rem / a.mj) * a.mj;
+      pix = ((int64_t)b * a.ho + a.oy0 + a.osy * i) * a.wo + a.ox0 + a.osx * j;
+    }
+    // the epilogue operands, before the first next-tile load
+    u32x2 oo[TN][4];
+    // GDN g = x at channel n = 32j + 8k + 4lh + e: K step 2j + k/2, fragment half k & 1, elements 4lh..
+    auto gx = [&](int j0) __attribute__((always_inline)) {
+      const int partner = (lane ^ 32) << 2;
+#pragma unroll
+      for (int j = j0; j < j0 + 3; ++j)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const u32x4 x = xc[2 * j + h2];
+          const unsigned own0 = lh ? x[2] : x[0], own1 = lh ? x[3] : x[1];
+          const unsigned rc0 = (unsigned)__builtin_amdgcn_ds_bpermute(partner, (int)(lh ? x[0] : x[2]));
+          const unsigned rc1 = (unsigned)__builtin_amdgcn_ds_bpermute(partner, (int)(lh ? x[1] : x[3]));
+          const u32x2 own = {own0, own1}, rcv = {rc0, rc1};
+          oo[j][2 * h2] = lh ? rcv : own;
+          oo[j][2 * h2 + 1] = lh ? own : rcv;
+        }
+    };
+    if constexpr (FAST == 2) {
+      // the first half's g now; the second half's after the K loop (its K steps 6..11 are re-loaded for the
+      // next tile only then): 24 live registers through the loop instead of 48
+      gx(0);
+    } else {
+      if (r1g) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) oo[j][k] = *(const u32x2*)(r1g + pix * a.ldr1 + n0 + j * 32 + 8 * k + 4 * lh);
+      }
+    }
+    floatx16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const bool more = tn < p.ntiles;
+    const unsigned vn = more ? voff(tn) : 0x80000000u;
+    int wl = wlane;
+    asm volatile("" : "+v"(wl));
+#pragma unroll
+    for (int kk = 0; kk < KST; ++kk) {
+      const u32x4 xv = PRO == LIC_PRO_SQUARE ? square(xc[kk]) : xc[kk];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const u32x4 wf = *(const u32x4*)(smem + wl + (kk * BN + j * 32) * 32);
+        acc[j] = mfma_k16<T>(wf, xv, acc[j]);
+      }
+      if (more && (FAST != 2 || kk < KST / 2)) xc[kk] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vn, kk * 32, 0);
+    }
+    if constexpr (FAST == 2) {
+      gx(3);
+      if (more) {
+#pragma unroll
+        for (int kk = KST / 2; kk < KST; ++kk) xc[kk] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vn, kk * 32, 0);
+      }
+    }
+    // register epilogue, one 96-channel half at a time through the wave's slot
+    const int epi = a.epi, act = a.act;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        const int j = 3 * hh + jj;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const floatx4 bv = *(const floatx4*)(sbias + j * 32 + 8 * k + 4 * lh);
+          float w[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = acc[j][4 * k + e] + bv[e];
+          if constexpr (FAST == 2) {
+            const T* ge = (const T*)&oo[j][k];
+            const bool sq = epi == LIC_EPI_GDN_SQRT;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float rs = __builtin_amdgcn_rsqf(w[e]);
+              w[e] = to_f(ge[e]) * (sq ? w[e] * rs : rs);
+            }
+          } else {
+            if (act == LIC_ACT_GELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] = gelu_f(w[e]);
+            } else if (act == LIC_ACT_LRELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : w[e] * a.slope;
+            } else if (act == LIC_ACT_RELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] = w[e] > 0.f ? w[e] : 0.f;
+            }
+            if (r1g) {
+              const T* re = (const T*)&oo[j][k];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] += to_f(re[e]);
+            }
+          }
+          u32x2 raw;
+          T* o = (T*)&raw;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = from_f<T>(w[e]);
+          *(u32x2*)(stg + l32 * 208 + (jj * 32 + 8 * k + 4 * lh) * 2) = raw;
+        }
+      }
+      if (lh == 0) ((int64_t*)(stg + 32 * 208))[l32] = pok ? pix : -1;
+      wave_lds_sync();
+#pragma unroll
+      for (int h = 0; h < 6; ++h) {
+        const int idx = lane + 64 * h, pr = idx / 12, c = idx - pr * 12;
+        const u32x4 val = *(const u32x4*)(stg + pr * 208 + c * 16);
+        const int64_t dp = ((const int64_t*)(stg + 32 * 208))[pr];
+        if (dp >= 0) {
+          *(u32x4*)(yg + dp * a.ldy + n0 + 96 * hh + c * 8) = val;
+          if (y2g) *(u32x4*)(y2g + dp * a.ldy2 + n0 + 96 * hh + c * 8) = val;
+        }
+      }
+      wave_lds_sync();
+    }
+    t = tn;
+  }
+}
+
 template <typename T, int BN, int KST, int PRO, int KT>
 void launch_g16(const lic_conv_args& a, const G16Plan& p, dim3 grid, int smem, hipStream_t s, int& status) {
   auto kern = p.fast_epi == 1 ? gemm16_kernel<T, BN, KST, PRO, KT, 1> : gemm16_kernel<T, BN, KST, PRO, KT, 0>;
@@ -391,6 +601,34 @@ int try_gemm16(const lic_conv_args& a, hipStream_t s, int& status) {
   p.fast_epi = g16_fast_epi_ok(a) && wd_env("LIC_G16_FAST_EPI", 1) ? 1 : 0;
   if (p.fast_epi && g16_gx_ok(a) && wd_env("LIC_G16_GX", 1)) p.fast_epi = 2;
   dim3 grid((unsigned)(wgs * p.nblk));
+  // the wide variant (gemm16w_kernel): 192-channel blocks of a 1x1, register epilogue with at most one
+  // operand set (r1, or GDN's g = x); LIC_G16_WIDE=0 restores the two-waves-per-tile kernel (A/B)
+  if constexpr (KT == 1 && BN == 192 && (KST == 12 || KST == 6)) {
+    static const int wide_on = wd_env("LIC_G16_WIDE", 1);
+    const bool gdn = a.g != nullptr;
+    if (wide_on && ((p.fast_epi == 1 && !gdn) || (p.fast_epi == 2 && a.r1 == nullptr))) {
+      int wg2 = 256 / p.nblk;
+      if (wg2 < 1) wg2 = 1;
+      const int need2 = (p.ntiles + 7) / 8;
+      if (wg2 > need2) wg2 = need2;
+      p.wgs = wg2;
+      const int smem2 = KST * BN * 32 + BN * 4 + 8 * G16_SLOT;
+      const dim3 grid2((unsigned)(wg2 * p.nblk));
+      auto kern = p.fast_epi == 2 ? (a.prologue == LIC_PRO_SQUARE ? gemm16w_kernel<T, KST, LIC_PRO_SQUARE, 2>
+                                                                  : gemm16w_kernel<T, KST, LIC_PRO_NONE, 2>)
+                                  : (a.prologue == LIC_PRO_SQUARE ? gemm16w_kernel<T, KST, LIC_PRO_SQUARE, 1>
+                                                                  : gemm16w_kernel<T, KST, LIC_PRO_NONE, 1>);
+      const hipError_t ea = ensure_dyn_lds((const void*)kern, smem2);
+      if (ea != hipSuccess) {
+        status = fail(std::string("gemm16w: dynamic LDS attribute: ") + hipGetErrorString(ea));
+        return 1;
+      }
+      hipLaunchKernelGGL(kern, grid2, dim3(512), smem2, s, a, p);
+      hipError_t e = hipGetLastError();
+      status = e == hipSuccess ? 0 : fail(std::string("gemm16w launch: ") + hipGetErrorString(e));
+      return 1;
+    }
+  }
   if constexpr (KT > 1) launch_g16<T, BN, KST, LIC_PRO_NONE, KT>(a, p, grid, smem, s, status);
   else if (a.prologue == LIC_PRO_SQUARE) launch_g16<T, BN, KST, LIC_PRO_SQUARE, 1>(a, p, grid, smem, s, status);
   else launch_g16<T, BN, KST, LIC_PRO_NONE, 1>(a, p, grid, smem, s, status);

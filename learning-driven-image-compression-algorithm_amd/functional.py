@@ -33,6 +33,27 @@ def stream_handle() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+_AUX_STREAMS = {}
+
+
+def aux_stream(device, key: str) -> "torch.cuda.Stream":
+    """A per-(device, key) side stream for an independent branch of a block (Win_noShift_Attention's /
+    SWAtten's conv_a).  Callers fork it from the capture stream only -- one level deep: a stream forked
+    from a side stream segfaults in hipGraph capture_end (tools/capture_fork_probe.py)."""
+    k = (str(device), key)
+    st = _AUX_STREAMS.get(k)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _AUX_STREAMS[k] = st
+    return st
+
+
+def fork_enabled() -> bool:
+    """conv_a of the 16x16-latent Win_noShift_Attention / the slice loop's mean SWAtten on a side stream
+    (LIC_FORK_CONV_A=0: on the current stream, for A/B)."""
+    return os.environ.get("LIC_FORK_CONV_A", "1") != "0"
+
+
 def _lib():
     return _ffi.load()
 

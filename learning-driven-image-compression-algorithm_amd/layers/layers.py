@@ -4,6 +4,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
+from .. import functional as Fn
 from ..functional import Act
 from ._conv import Conv2d
 from .compressai import ResidualBlock
@@ -43,13 +44,25 @@ class Win_noShift_Attention(nn.Module):
             wba(), conv1x1(N, N), wba(), ResidualBlock(N, N), conv3x3(N, N), wba(), ResidualBlock(N, N),
             conv7x7(N, N), wba(), ResidualBlock(N, N))
 
-    def run(self, x: Act, out: Optional[Act] = None) -> Act:
-        # (conv_a on a side stream, concurrent with conv_b, was tried on the 16x16 latents: a hipGraph
-        # capture of the slice loop's stream fork with this one nested in it segfaults in
-        # capture_end with plain torch kernels too -- tools/capture_fork_probe.py)
-        a = x
-        for blk in self.conv_a:
-            a = blk.run(a)
+    def run(self, x: Act, out: Optional[Act] = None, fork: bool = False) -> Act:
+        """fork=True (the 16x16 latents of the a_model / s_model, called on the capture stream): conv_a runs
+        on a side stream forked from the current one and joined before the gate, concurrent with conv_b's
+        chain -- both are chains of latency-bound launches there.  One level only: the caller guarantees the
+        current stream is the capture stream (a nested fork segfaults in hipGraph capture,
+        tools/capture_fork_probe.py)."""
+        side = None
+        if fork and Fn.fork_enabled():
+            main = torch.cuda.current_stream(x.t.device)
+            side = Fn.aux_stream(x.t.device, "conv_a")
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                a = x
+                for blk in self.conv_a:
+                    a = blk.run(a)
+        else:
+            a = x
+            for blk in self.conv_a:
+                a = blk.run(a)
         b = self.conv_b[0].run(x)
         b = self.conv_b[1].run(b)
         b = self.conv_b[2].run(b)
@@ -59,6 +72,9 @@ class Win_noShift_Attention(nn.Module):
         b = self.conv_b[6].run(b)
         b = self.conv_b[7].run(b)
         b = self.conv_b[8].run(b)
+        if side is not None:
+            main.wait_stream(side)
+            a.t.record_stream(main)     # allocated on the side stream, read by the gate on this one
         return self.conv_b[9].run(b, out, gate_a=a, gate_r=x)
 
     def forward(self, x):

@@ -129,18 +129,33 @@ class SWAtten(AttentionBlock):
             self.in_conv = conv1x1(input_dim, inter_dim)
             self.out_conv = conv1x1(inter_dim, output_dim)
 
-    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+    def run(self, x: Act, out: Optional[Act] = None, fork: bool = False) -> Act:
+        """fork=True (the slice loop's mean branch, on the capture stream): conv_a (3 ResidualUnits on x)
+        on a side stream forked from the current one -- a sibling of the scale branch's stream --, concurrent
+        with the Swin chain that feeds conv_b.  The scale branch (itself on a side stream) keeps conv_a in
+        order: forking from a side stream nests the fork, which segfaults in hipGraph capture
+        (tools/capture_fork_probe.py)."""
         x = self.in_conv.run(x)
-        # conv_a (3 ResidualUnits on x) and the Swin chain that feeds conv_b run in order on the
-        # current stream: forking conv_a to a stream of its own nests that fork inside the slice
-        # loop's, and hipGraph capture of the nested fork segfaults (tools/capture_fork_probe.py)
-        a = x
-        for u in self.conv_a:
-            a = u.run(a)
+        side = None
+        if fork and Fn.fork_enabled():
+            main = torch.cuda.current_stream(x.t.device)
+            side = Fn.aux_stream(x.t.device, "conv_a")
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                a = x
+                for u in self.conv_a:
+                    a = u.run(a)
+        else:
+            a = x
+            for u in self.conv_a:
+                a = u.run(a)
         z = self.non_local_block.run(x)
         b = z
         for u in list(self.conv_b)[:3]:
             b = u.run(b)
+        if side is not None:
+            main.wait_stream(side)
+            a.t.record_stream(main)
         g = self.conv_b[3].run(b, epi=EPI_GATE, g=a, r2=x)
         return self.out_conv.run(g, out)
 
@@ -187,7 +202,7 @@ class analysisTransformModel(nn.Module):
         x = t[12].run(x)
         x = t[13].run(x)
         x = t[15].run(x, pad=(1, 1, 2, 2))
-        return t[16].run(x, out)
+        return t[16].run(x, out, fork=True)   # (the 16x16 latents: conv_a concurrent with conv_b)
 
     def _rb3_chain_params(self):
         blocks = [self.transform[i] for i in range(3)]
@@ -226,7 +241,7 @@ class synthesisTransformModel(nn.Module):
 
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
         t = self.transform
-        x = t[0].run(x)
+        x = t[0].run(x, fork=True)   # (the 16x16 latents: conv_a concurrent with conv_b)
         x = t[2].run(x, prepad=(1, 1))
         x = t[3].run(x)
         x = t[5].run(x, prepad=(1, 1))
@@ -561,7 +576,7 @@ class Net(nn.Module):
                 t = cs[0].run(ss, act=ACT_GELU)
                 t = cs[2].run(t, act=ACT_GELU)
                 sc = cs[4].run(t, out=SC.ch(sw * i, sw * (i + 1)))
-            ms = self.atten_mean[i][0].run(MS.ch(0, ci), out=LR.ch(0, ci))
+            ms = self.atten_mean[i][0].run(MS.ch(0, ci), out=LR.ch(0, ci), fork=True)
             cm = self.cc_mean_transforms[i]
             t = cm[0].run(ms, act=ACT_GELU)
             t = cm[2].run(t, act=ACT_GELU)
