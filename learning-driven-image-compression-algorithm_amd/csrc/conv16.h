@@ -34,7 +34,9 @@ typedef __attribute__((address_space(3))) void c16_lds_void;
 #ifndef C16_STAMP
 #define C16_STAMP 0
 #endif
-// diagnostic ablations (-DC16_ABL=bits, timing only, outputs wrong): 1 no stores in the register epilogue
+// diagnostic ablations (-DC16_ABL=bits, timing only, outputs wrong): 1 no stores in the register epilogue,
+// 2 every chunk's halo read from chunk 0 (L2-resident after the first stage), 4 no weight DMA after the
+// prologue, 8 no halo DMA after the prologue
 #ifndef C16_ABL
 #define C16_ABL 0
 #endif
@@ -257,14 +259,14 @@ __global__ __launch_bounds__(512, 1) void conv16_kernel(const lic_conv_args a, c
   auto issue_piece = [&](int m, int k, int g, int hb, int wb, bool with_halo) {
     // m < HPW: halo piece m; else weight piece m - HPW
     if (m < HPW) {
-      if (!with_halo) return;
+      if (!with_halo || ((C16_ABL & 8) && (k | g) != 0)) return;
       const int P = wave + NW * m;
       if (P >= Geo::HPIECES) return;
       const unsigned ho = S == 1 ? hoff[S == 1 ? m : 0] : halo_off(m, g >> 1, g & 1);
-      c16_dma(xrs, smem + hb * HBYTES + P * 1024, ho, k * 32);
+      c16_dma(xrs, smem + hb * HBYTES + P * 1024, ho, (C16_ABL & 2) ? 0 : k * 32);
     } else {
       const int Q = wq0 + NW * (m - HPW);
-      if (Q >= Geo::WPIECES) return;
+      if (Q >= Geo::WPIECES || ((C16_ABL & 4) && (k | g) != 0)) return;
       const int tt = Q / (BN / 32), nq = Q - tt * (BN / 32);
       int tap;
       if constexpr (S == 1) {
