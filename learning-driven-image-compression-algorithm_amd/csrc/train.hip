@@ -14,6 +14,7 @@
 #include "lic_common.h"
 
 namespace lic {
+int wd_env(const char* name, int def);   // conv_split_wd.hip
 
 // ---------------------------------------------------------------------------- wgrad
 // Operand staging: a "unit" is EPC pixels x EPC channels (EPC = 16 B / element).
@@ -613,6 +614,216 @@ __global__ __launch_bounds__(256) void win_attn_bwd_kernel(const lic_attn_args a
     for (int r = tid; r < R; r += 256) tparts[((int64_t)h * nwin + win) * R + r] = stab[r];
 }
 
+// The 8x8-window case (N = 64 tokens, head dim D a multiple of 4: the a_model / s_model WBA at 64^2 and
+// the slice loop's WMSA), round 6: the same math as win_attn_bwd_kernel with the O(N^2 d) products
+// register-blocked -- each of the 256 threads owns a 4 x 4 block of (query i, key j) = (ib + 16 r,
+// jb + 16 s), so one q / k row read (float4 along d) feeds 4 products instead of 1 and the 16 keys of a
+// block row sit in 16 consecutive lanes (row max / sum / D by xor-shuffles); dP = dO V^T is computed
+// ONCE (the generic kernel computes it twice, the D pass on 64 threads of 1536 serial products each);
+// the table row of the head sits in LDS.  The dot products keep the generic kernel's order (sequential
+// over the channel); the softmax sum and D are summed in a butterfly: last-bit differences from it.
+template <typename T, int D>
+__global__ __launch_bounds__(256) void win_attn_bwd64_kernel(const lic_attn_args a, const T* __restrict__ dout,
+                                                             int lddo, T* __restrict__ dqkv, int lddq,
+                                                             float* __restrict__ tparts) {
+  constexpr int WS = 8, N = 64, DP = D + 4, R = 225, NP = N + 1, DC = D / 4;
+  const int nwx = a.w / WS, nwy = a.h / WS;
+  int bid = blockIdx.x;
+  const int h = bid % a.heads;
+  bid /= a.heads;
+  const int win = bid;
+  const int wx = bid % nwx;
+  bid /= nwx;
+  const int wy = bid % nwy;
+  const int b = bid / nwy;
+  const int nwin = a.n * nwy * nwx;
+
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* sq = sm;                 // [N][DP]
+  float* sk = sq + N * DP;
+  float* sv = sk + N * DP;
+  float* sdo = sv + N * DP;
+  float* sP = sdo + N * DP;       // [N][NP]  P
+  float* sS = sP + N * NP;        // [N][NP]  dS
+  float* sbt = sS + N * NP;       // [R] this head's bias table
+  float* stab = sbt + R;          // [R] table-gradient partials
+  const int tid = threadIdx.x;
+
+  auto pix = [&](int t) -> int64_t {
+    const int sy = wy * WS + t / WS, sx = wx * WS + t % WS;
+    int py = sy + a.shift, px = sx + a.shift;
+    if (py >= a.h) py -= a.h;
+    if (px >= a.w) px -= a.w;
+    return ((int64_t)b * a.h + py) * a.w + px;
+  };
+  const T* qkv = (const T*)a.qkv;
+  for (int e = tid; e < N * D; e += 256) {
+    const int t = e / D, c = e % D;
+    const int64_t p = pix(t);
+    const T* q = qkv + p * a.ldqkv + h * D + c;
+    sq[t * DP + c] = to_f(q[0]);
+    sk[t * DP + c] = to_f(q[a.c]);
+    sv[t * DP + c] = to_f(q[2 * a.c]);
+    sdo[t * DP + c] = to_f(dout[p * lddo + h * D + c]);
+  }
+  for (int r = tid; r < R; r += 256) sbt[r] = a.table[r * a.tab_sr + h * a.tab_sh];
+  __syncthreads();
+
+  const float scale = a.scale;
+  const int ib = tid >> 4, jb = tid & 15;
+  const int split = WS - a.shift;
+  const bool last_row = (wy == nwy - 1), last_col = (wx == nwx - 1);
+  auto reg_wba = [&](int y, int x) {
+    const int ly = y < a.h - WS ? 0 : (y < a.h - a.shift ? 1 : 2);
+    const int lx = x < a.w - WS ? 0 : (x < a.w - a.shift ? 1 : 2);
+    return ly * 3 + lx;
+  };
+  // ---- scores, P = softmax (rows i = ib + 16 r, keys j = jb + 16 s) ----
+  float P[4][4], G[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) P[r][s2] = G[r][s2] = 0.f;
+  for (int c = 0; c < D; c += 4) {
+    float4 qr[4], kr[4], dr[4], vr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      qr[r] = *(const float4*)(sq + (ib + 16 * r) * DP + c);
+      dr[r] = *(const float4*)(sdo + (ib + 16 * r) * DP + c);
+      kr[r] = *(const float4*)(sk + (jb + 16 * r) * DP + c);
+      vr[r] = *(const float4*)(sv + (jb + 16 * r) * DP + c);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float q4[4] = {qr[r].x, qr[r].y, qr[r].z, qr[r].w};
+      const float d4[4] = {dr[r].x, dr[r].y, dr[r].z, dr[r].w};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const float k4[4] = {kr[s2].x, kr[s2].y, kr[s2].z, kr[s2].w};
+        const float v4[4] = {vr[s2].x, vr[s2].y, vr[s2].z, vr[s2].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float qv = a.scale_after ? q4[e] : q4[e] * scale;
+          P[r][s2] += qv * k4[e];          // the generic kernel's order: sequential over the channel
+          G[r][s2] += d4[e] * v4[e];       // dP = dO . v
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = ib + 16 * r, iy = i / WS, ix = i % WS;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int j = jb + 16 * s2, jy = j / WS, jx = j % WS;
+      float dot = P[r][s2];
+      if (a.scale_after) dot = dot * scale;
+      float v = dot + sbt[(iy - jy + WS - 1) * (2 * WS - 1) + (ix - jx + WS - 1)];
+      if (a.mask_kind == 1) {
+        if (reg_wba(wy * WS + jy, wx * WS + jx) != reg_wba(wy * WS + iy, wx * WS + ix)) v += -100.0f;
+      } else if (a.mask_kind == 2) {
+        bool m = false;
+        if (last_row && ((iy < split) != (jy < split))) m = true;
+        if (last_col && ((ix < split) != (jx < split))) m = true;
+        if (m) v = -INFINITY;
+      }
+      P[r][s2] = v;
+    }
+    float mx = fmaxf(fmaxf(P[r][0], P[r][1]), fmaxf(P[r][2], P[r][3]));
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      P[r][s2] = expf(P[r][s2] - mx);
+      sum += P[r][s2];
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.0f / sum;
+    float dsum = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      P[r][s2] *= inv;
+      dsum += P[r][s2] * G[r][s2];
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) dsum += __shfl_xor(dsum, o);   // D_i = sum_j P_ij dP_ij
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int j = jb + 16 * s2;
+      sP[i * NP + j] = P[r][s2];
+      sS[i * NP + j] = P[r][s2] * (G[r][s2] - dsum);   // dS
+    }
+  }
+  __syncthreads();
+  // ---- table gradient: every relative offset sums its (i, j) pairs of dS in a fixed order ----
+  for (int r = tid; r < R; r += 256) {
+    const int dy = r / (2 * WS - 1) - (WS - 1), dx = r % (2 * WS - 1) - (WS - 1);
+    float acc = 0.f;
+    for (int iy = max(0, dy); iy < min(WS, WS + dy); ++iy)
+      for (int ix = max(0, dx); ix < min(WS, WS + dx); ++ix)
+        acc += sS[(iy * WS + ix) * NP + (iy - dy) * WS + (ix - dx)];
+    stab[r] = acc;
+  }
+  // ---- dV_j = sum_i P_ij dO_i, dQ_i = scale sum_j dS_ij k_j, dK_j = scale sum_i dS_ij q_i (sequential
+  // over i / j as the generic kernel); thread = (token t = tid / 4, channel quarter) ----
+  {
+    const int t = tid >> 2, c0 = (tid & 3) * DC;
+    float av[DC], aq[DC], ak[DC];
+#pragma unroll
+    for (int e = 0; e < DC; ++e) av[e] = aq[e] = ak[e] = 0.f;
+    for (int u = 0; u < N; ++u) {
+      const float pt = sP[u * NP + t];        // P_{u t}: key t of query u
+      const float st = sS[u * NP + t];        // dS_{u t}
+      const float su = sS[t * NP + u];        // dS_{t u}
+#pragma unroll
+      for (int e = 0; e < DC; ++e) {
+        av[e] += pt * sdo[u * DP + c0 + e];
+        aq[e] += su * sk[u * DP + c0 + e];
+        ak[e] += st * sq[u * DP + c0 + e];
+      }
+    }
+    const int64_t p = pix(t);
+#pragma unroll
+    for (int e = 0; e < DC; ++e) {
+      dqkv[p * lddq + 2 * a.c + h * D + c0 + e] = from_f<T>(av[e]);
+      dqkv[p * lddq + h * D + c0 + e] = from_f<T>(aq[e] * scale);
+      dqkv[p * lddq + a.c + h * D + c0 + e] = from_f<T>(ak[e] * scale);
+    }
+  }
+  if (tparts) {
+    __syncthreads();
+    for (int r = tid; r < R; r += 256) tparts[((int64_t)h * nwin + win) * R + r] = stab[r];
+  }
+}
+
+// Deterministic second pass of the table gradient, round 6: block (head, 16 offsets) x 16 window slices --
+// slice w sums windows w, w + 16, ... in order, then the 16 slice sums are added in order (a fixed tree:
+// the one-thread-per-offset loop over all windows ran 7 workgroups for up to 180 us).
+__global__ __launch_bounds__(256) void attn_table_reduce16_kernel(const float* __restrict__ parts, int heads,
+                                                                  int nwin, int R, float* __restrict__ dtab,
+                                                                  int tab_sr, int tab_sh, int accumulate) {
+  __shared__ float red[16][17];
+  const int rl = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int nrb = (R + 15) / 16;
+  const int h = blockIdx.x / nrb, r = (blockIdx.x % nrb) * 16 + rl;
+  float acc = 0.f;
+  if (r < R) {
+    const float* pp = parts + (int64_t)h * nwin * R + r;
+    for (int k = sl; k < nwin; k += 16) acc += pp[(int64_t)k * R];
+  }
+  red[sl][rl] = acc;
+  __syncthreads();
+  if (sl == 0 && r < R) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][rl];
+    float* o = dtab + r * tab_sr + h * tab_sh;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
 __global__ void attn_table_reduce_kernel(const float* __restrict__ parts, int heads, int nwin, int R,
                                          float* __restrict__ dtab, int tab_sr, int tab_sh, int accumulate) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1151,13 +1362,35 @@ extern "C" int lic_win_attn_bwd(const lic_attn_args* ap, const void* dout, int32
   const int64_t blocks = (int64_t)nwin * a.heads;
   hipStream_t s = (hipStream_t)stream;
   float* tp = dtable ? ws : nullptr;
-  TR_DISPATCH(a.dtype, "attn_bwd",
-              hipLaunchKernelGGL(win_attn_bwd_kernel<T>, dim3((unsigned)blocks), dim3(256), shm, s, a,
-                                 (const T*)dout, lddo, (T*)dqkv, lddq, tp));
+  // 8x8 windows with a head dim of 16 / 24 / 32: the register-blocked kernel (LIC_ATTN_BWD64=0: generic)
+  static const int blk_on = wd_env("LIC_ATTN_BWD64", 1);
+  bool done = false;
+  if (blk_on && N == 64 && (d == 16 || d == 24 || d == 32)) {
+    const size_t shm64 = (size_t)(4 * 64 * (d + 4) + 2 * 64 * 65 + 2 * 225) * sizeof(float);
+#define ATTN64(DD)                                                                                             \
+  if (d == DD) {                                                                                                 \
+    TR_DISPATCH(a.dtype, "attn_bwd64", {                                                                        \
+      const hipError_t ea = ensure_dyn_lds((const void*)win_attn_bwd64_kernel<T, DD>, (int)shm64);             \
+      if (ea != hipSuccess) return fail(std::string("attn_bwd64: dynamic LDS: ") + hipGetErrorString(ea));      \
+      hipLaunchKernelGGL((win_attn_bwd64_kernel<T, DD>), dim3((unsigned)blocks), dim3(256), shm64, s, a,         \
+                         (const T*)dout, lddo, (T*)dqkv, lddq, tp);                                            \
+    });                                                                                                          \
+    done = true;                                                                                                 \
+  }
+    ATTN64(16)
+    ATTN64(24)
+    ATTN64(32)
+#undef ATTN64
+  }
+  if (!done)
+    TR_DISPATCH(a.dtype, "attn_bwd",
+                hipLaunchKernelGGL(win_attn_bwd_kernel<T>, dim3((unsigned)blocks), dim3(256), shm, s, a,
+                                   (const T*)dout, lddo, (T*)dqkv, lddq, tp));
   LIC_CHECK_LAUNCH();
   if (dtable) {
-    hipLaunchKernelGGL(attn_table_reduce_kernel, dim3((a.heads * R + 255) / 256), dim3(256), 0, s, ws, a.heads, nwin,
-                       R, dtable, a.tab_sr, a.tab_sh, accumulate_table);
+    const int nrb = (R + 15) / 16;
+    hipLaunchKernelGGL(attn_table_reduce16_kernel, dim3((unsigned)(a.heads * nrb)), dim3(256), 0, s, ws, a.heads,
+                       nwin, R, dtable, a.tab_sr, a.tab_sh, accumulate_table);
     LIC_CHECK_LAUNCH();
   }
   return 0;

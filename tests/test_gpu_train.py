@@ -259,7 +259,7 @@ def _attn_core_ref(qkv, table, C, heads, ws, shift, wmsa):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("ws,shift,wmsa,C", [(8, 4, False, 192), (8, 0, False, 64), (4, 2, False, 64),
+@pytest.mark.parametrize("ws,shift,wmsa,C", [(8, 4, False, 192), (8, 0, False, 64), (4, 2, False, 64), (8, 2, False, 256),
                                              (2, 1, False, 64), (8, 4, True, 128), (8, 0, True, 128)])
 def test_win_attn_grad(dtype, ws, shift, wmsa, C):
     from lic_amd import autograd as AG
