@@ -361,6 +361,55 @@ def a_model_rate(net, x, dtype, iters=10):
     return time_graph(ga, iters)
 
 
+def conv_stack_roofline(net, x, dtype, peak, reps=10):
+    """The analysis transform's convolution stack, kernel by kernel: every top-level convolution launch of
+    one a_model pass (k x k and 1x1 incl. GDN's x^2-Gamma 1x1 and the proj Linears; NOT the fused qkv +
+    window-attention launch, the ResidualBottleneck(3) chain or elementwise work) is replayed alone from a
+    hipGraph of `reps` copies on its recorded operands; FLOPs = 2 x output pixels x co x ci x taps
+    (SURVEY.md 8(d)).  A kernel-level figure beside the whole-a_model fraction, which also pays for the
+    attention, the launch boundaries and the overlap of nothing with nothing."""
+    import lic_amd.functional as Fn
+    from lic_amd.functional import Act, split_f32
+    calls, depth = [], [0]
+    orig = Fn.conv
+
+    def rec(xa, pk, out=None, **kw):
+        top = depth[0] == 0
+        depth[0] += 1
+        try:
+            res = orig(xa, pk, out, **kw)
+        finally:
+            depth[0] -= 1
+        if top:
+            calls.append((xa, pk, res, kw))
+        return res
+    xin = Act(x.to(dtype).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1))
+    Fn.conv = rec
+    try:
+        with torch.no_grad(), split_f32(SPLIT_MODES.get(net.precision, 0)):
+            net.a_model.run(xin)
+    finally:
+        Fn.conv = orig
+    torch.cuda.synchronize()
+    tot_t = tot_f = 0.0
+    with torch.no_grad(), split_f32(SPLIT_MODES.get(net.precision, 0)):
+        for xa, pk, res, kw in calls:
+            def once(xa=xa, pk=pk, res=res, kw=kw):
+                for _ in range(reps):
+                    orig(xa, pk, res, **kw)
+            g, _ = capture(once, warm=1)
+            t = time_graph(g, 3) / reps
+            tot_t += t
+            tot_f += 2.0 * res.B * res.H * res.W * pk.co * pk.ci * len(pk.dy)
+            del g
+    tf = tot_f / tot_t / 1e12
+    return {"launches": len(calls), "gflop_per_batch": round(tot_f / 1e9, 1), "ms": round(tot_t * 1e3, 3),
+            "tflops": round(tf, 2), "frac_of_peak": round(tf / peak, 4),
+            "note": "every top-level convolution launch of one a_model pass replayed alone (hipGraph of "
+                    f"{reps} copies, HIP-event-free wall clock of 3 replays); excludes the fused qkv + window "
+                    "attention, the ResidualBottleneck(3) chain and elementwise launches"}
+
+
 def extra_leg(args, other, x, device, gf_a):
     """Another precision on the same workload: forward rate, parity at the bench batch, a_model
     and the dominant-kernel roofline."""
@@ -375,6 +424,7 @@ def extra_leg(args, other, x, device, gf_a):
     leg = {"value": round(args.batch / t2, 2), "unit": "images/s", "ms_per_step": round(t2 * 1e3, 3),
            "parity": parity_check(args.arch, other, args.size, device, args.batch),
            "a_model": {"ms": round(ta2 * 1e3, 3), "tflops": round(a2, 2), "frac_of_peak": round(a2 / peak2, 4)},
+           "a_model_conv_stack": conv_stack_roofline(net2, x, odt, peak2),
            "roofline": {"achieved": round(f2 / tk2 / 1e12, 2), "peak": peak2,
                         "frac": round(f2 / tk2 / 1e12 / peak2, 4),
                         "traffic": _pmc_traffic(("split", split) if split else odt, args.batch, args.size),
@@ -548,6 +598,7 @@ def main():
             "a_model": {"ms": round(ta * 1e3, 3), "images_per_s": round(args.batch / ta, 2),
                         "tflops": round(a_tflops, 2), "frac_of_peak": round(a_tflops / peak, 4),
                         "gflop_per_image": gf_a},
+            "a_model_conv_stack": conv_stack_roofline(net, x, dtype, peak),
             "full_forward_tflops": round(FULL_GFLOP_256 * (args.size / 256) ** 2 * value / world / 1e3, 2),
             "graph_nodes_per_step": None if args.no_graph else graph_nodes(graph),
         }

@@ -48,6 +48,16 @@ def aux_stream(device, key: str) -> "torch.cuda.Stream":
     return st
 
 
+def chains_for(B: int) -> int:
+    """How many independent image chains the analysis transform runs concurrently (LIC_CHAINS, default 1):
+    half-batches on two streams, so one chain's prologue / epilogue-bound phases could overlap the other
+    chain's MFMA-bound main loops (images are independent; the arithmetic per image is unchanged).  Measured
+    on MI355X at B=32, 256^2 (profiles/r06/chains_ab.txt): fp16 a_model 3.813 -> 3.874 ms, fp32x6 14.097 ->
+    14.008 ms -- the half-batch launches lose more than the overlap wins, so it stays an opt-in A/B."""
+    n = int(os.environ.get("LIC_CHAINS", "1"))
+    return n if (n > 1 and B >= 2 * n) else 1
+
+
 def fork_enabled() -> bool:
     """conv_a of the 16x16-latent Win_noShift_Attention / the slice loop's mean SWAtten on a side stream
     (LIC_FORK_CONV_A=0: on the current stream, for A/B)."""
@@ -111,6 +121,10 @@ class Act:
     def ch(self, a: int, b: int) -> "Act":
         assert 0 <= a <= b <= self.c
         return Act(self.t, self.c0 + a, b - a)
+
+    def batch(self, b0: int, b1: int) -> "Act":
+        """Images [b0, b1) of this view (the batch is the outermost dimension: still contiguous)."""
+        return Act(self.t[b0:b1], self.c0, self.c, self.zpad)
 
     def nchw(self) -> torch.Tensor:
         """Logical NCHW tensor (channels_last storage) of this view."""

@@ -164,6 +164,26 @@ class SWAtten(AttentionBlock):
 
 
 # --------------------------------------------------------------------------- transforms
+def run_chains(x: Act, out: Act, n: int, body) -> Act:
+    """body(x_i, out_i, fork) on n image chains: chain 0 on the current stream, chains 1.. on side streams
+    forked from it and joined back (never nested: the chains' own forks are off)."""
+    main = torch.cuda.current_stream(x.t.device)
+    cuts = [x.B * i // n for i in range(n + 1)]
+    sides = [Fn.aux_stream(x.t.device, f"chain{i}") for i in range(1, n)]
+    for s in sides:
+        s.wait_stream(main)
+    for i in range(n):
+        xi, oi = x.batch(cuts[i], cuts[i + 1]), out.batch(cuts[i], cuts[i + 1])
+        if i == 0:
+            body(xi, oi, False)
+        else:
+            with torch.cuda.stream(sides[i - 1]):
+                body(xi, oi, False)
+    for s in sides:
+        main.wait_stream(s)
+    return out
+
+
 class analysisTransformModel(nn.Module):
     """Encoder g_a, net_ga.py:253-309."""
 
@@ -186,6 +206,18 @@ class analysisTransformModel(nn.Module):
         )
 
     def run(self, x: Act, out: Optional[Act] = None) -> Act:
+        """Called on the capture stream.  With Fn.chains_for(B) = n > 1 the batch runs as n independent image
+        chains, chain 0 on the current stream and the others on side streams forked from it (one level; their
+        inner conv_a forks are then off), joined before returning: each image sees the same launches'
+        arithmetic, the chains overlap one another's latency-bound phases."""
+        n = Fn.chains_for(x.B)
+        if n > 1 and x.H % 16 == 0 and x.W % 16 == 0:
+            if out is None:
+                out = Act.empty(x.B, x.H // 16, x.W // 16, self.transform[15].out_channels, x.dtype, x.t.device)
+            return run_chains(x, out, n, lambda xi, oi, fork: self._run(xi, oi, fork))
+        return self._run(x, out, True)
+
+    def _run(self, x: Act, out: Optional[Act], fork: bool) -> Act:
         t = self.transform
         if all(t[i].rb3_ok(x) for i in range(3)) and os.environ.get("LIC_RB3_CHAIN", "1") != "0":
             x = Fn.rb3_chain(x, self._rb3_chain_params(), 3)   # the three blocks in one launch
@@ -202,7 +234,7 @@ class analysisTransformModel(nn.Module):
         x = t[12].run(x)
         x = t[13].run(x)
         x = t[15].run(x, pad=(1, 1, 2, 2))
-        return t[16].run(x, out, fork=True)   # (the 16x16 latents: conv_a concurrent with conv_b)
+        return t[16].run(x, out, fork=fork)   # (the 16x16 latents: conv_a concurrent with conv_b)
 
     def _rb3_chain_params(self):
         blocks = [self.transform[i] for i in range(3)]

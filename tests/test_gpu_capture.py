@@ -48,3 +48,31 @@ def test_conv_a_fork_bitwise(precision, monkeypatch):
     g.replay()
     torch.cuda.synchronize()
     assert all(torch.equal(u, v) for u, v in zip(out, b[0]))
+
+
+@pytest.mark.parametrize("precision", ["fp32x6", "fp16"])
+def test_analysis_chains_match(precision, monkeypatch):
+    """LIC_CHAINS=2 (opt-in: two half-batches of the analysis transform on two streams, forked from the
+    current stream and joined back) computes the same latents as the single chain: images are independent,
+    only the launch split differs (a launch on a half-batch may pick another tiling, so equality is to
+    accumulation-order tolerance, not bitwise), and it captures into a hipGraph."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from lic_amd.functional import Act, split_f32
+    B, S = 8, 256
+    dt = torch.float16 if precision == "fp16" else torch.float32
+    net = bench.build_net("net_ga", precision, S, B, "cpu").cuda()
+    x = bench.bench_input(B, S, 0).cuda()
+    xin = Act(x.to(dt).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1))
+    ys = {}
+    with torch.no_grad(), split_f32(bench.SPLIT_MODES.get(precision, 0)):
+        for n in ("1", "2"):
+            monkeypatch.setenv("LIC_CHAINS", n)
+            ys[n] = net.a_model.run(xin).t.float().clone()
+        g, out = bench.capture(lambda: net.a_model.run(xin))
+        g.replay()
+    torch.cuda.synchronize()
+    ref = ys["1"]
+    tol = (2e-2 if precision == "fp16" else 1e-4) * ref.abs().max().item()
+    assert (ys["2"] - ref).abs().max().item() <= tol
+    assert torch.equal(out.t.float(), ys["2"])
