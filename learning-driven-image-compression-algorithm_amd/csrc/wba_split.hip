@@ -22,6 +22,8 @@
 
 namespace lic {
 
+int wd_env(const char* name, int def);   // conv_split_wd.hip
+
 namespace {
 
 constexpr int WB_C = 192, WB_HEADS = 8, WB_D = 24, WB_WS = 8, WB_T = 64;
@@ -43,6 +45,22 @@ __device__ __forceinline__ void split8(float4 lo, float4 hi, u32x4 (&out)[3]) {
 }
 
 }  // namespace
+
+// diagnostic build only (-DW6_STAMP=1, tools/wba_stamps.py): wave 0's per-phase cycle sums (s_memtime),
+// written past the end of the output (the caller allocates room); outputs stay valid
+#ifndef W6_STAMP
+#define W6_STAMP 0
+#endif
+#if W6_STAMP
+#define W6T(v)                                                                           \
+  do {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+  } while (0)
+#else
+#define W6T(v)
+#endif
 
 // Persistent: a workgroup per CU walks windows blockIdx.x, + gridDim.x, ...; the next window's
 // activations are loaded into registers before the current one's last attention phase (which issues no
@@ -76,8 +94,13 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
     }
   };
   if ((int)blockIdx.x < nwin) load_x(blockIdx.x);
+#if W6_STAMP
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0, t6 = 0, t7 = 0, te = 0;
+  unsigned long long s_a = 0, s_b0 = 0, s_gemm = 0, s_b1 = 0, s_s = 0, s_sm = 0, s_pv = 0, s_be = 0;
+#endif
 
   for (int win = blockIdx.x; win < nwin; win += gridDim.x) {
+    W6T(t0);
     floatx16 Ok0, Ok1;   // PROJ: this wave's attention output of head group 0 / 1 (head 4g + wave/2)
     const int wx = win % nwx, wy = (win / nwx) % nwy;
     // ---- phase A: the window's 64 x 192 fp32 activations -> three bf16 planes; 32-channel chunk k
@@ -94,6 +117,10 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
       }
     }
 
+    W6T(t1);
+#if W6_STAMP
+    s_a += t1 - t0;
+#endif
     const int nsteps = WB_C / 16;   // 12 sixteen-channel steps of the qkv reduction
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)a.qkv_wsplit, (short)0, (int)(18 * nsteps * 3 * 1024), 0x00020000);
@@ -101,66 +128,80 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
     for (int g = 0; g < 2; ++g) {   // head groups: heads 4g .. 4g+3
       // planes written (g = 0); the previous group's / window's attention done with qkv / tab
       __syncthreads();
+      W6T(t2);
 
-      // ---- phase B: qkv of the group, 2 token tiles x 9 column tiles (q, k, v x 3 of 32) = 18 tiles;
-      // wave w takes tiles w', w'+8, w'+16 (w' = w - 2g mod 8: the third tiles rotate between the
-      // groups, so every SIMD does the same work over the window); a wave's tiles share one token tile
-      const int wq = (wave - 2 * g) & 7;
-      const int mt = wq & 1;
-      auto gemm = [&](auto cnt_c) {
-        constexpr int CNT = decltype(cnt_c)::value;
-        int jt[CNT], which[CNT], sub[CNT];
+      // ---- phase B: qkv of the group, 2 token tiles x 9 column tiles (q, k, v x 3 of 32) = 18 tiles.
+      // Wave w owns local n-tile w for BOTH token tiles, so each weight fragment it loads from L2 feeds
+      // two MFMAs (a v1 assignment of one token tile per wave loaded every fragment twice per CU:
+      // profiles/r06/wba_f32x6_stamps_v1.txt, GEMM 47 % of the cycles); the ninth n-tile goes by token
+      // tile to waves 2g, 2g+1 (waves w and w + 4 share a SIMD: SIMDs 0, 1 take group 0's extra tiles
+      // and 2, 3 group 1's, so every SIMD does the same work over the window).  Per output tile the
+      // products and their order are v1's: bit-identical.
+      const bool ex = (wave >> 1) == g;
+      const int tx = wave & 1;
+      auto gemm = [&](auto exc) {
+        constexpr bool EX = decltype(exc)::value;
+        constexpr int NB = EX ? 2 : 1;   // n-tiles: this wave's, + local tile 8
+        int jt[NB], which[NB], sub[NB];
 #pragma unroll
-        for (int i = 0; i < CNT; ++i) {
-          const int nt = (wq + 8 * i) >> 1;
+        for (int i = 0; i < NB; ++i) {
+          const int nt = i == 0 ? wave : 8;
           which[i] = nt / 3;
           sub[i] = nt % 3;
           jt[i] = which[i] * 6 + 3 * g + sub[i];   // packed n-tile of qkv columns which*192 + 96g + 32*sub
         }
-        floatx16 acc[CNT];
+        floatx16 acc[2], accx;
 #pragma unroll
-        for (int i = 0; i < CNT; ++i)
+        for (int r = 0; r < 16; ++r) acc[0][r] = acc[1][r] = accx[r] = 0.f;
+        auto load_b = [&](int s, u32x4(&fb)[3][NB]) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-        const char* arow = xp + (32 * mt + lr) * (WB_XS * 2) + lh * 16;
-        auto load_b = [&](int s, u32x4(&fb)[3][CNT]) {
-#pragma unroll
-          for (int i = 0; i < CNT; ++i)
+          for (int i = 0; i < NB; ++i)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
               fb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, ((jt[i] * nsteps + s) * 3 + p) * 1024, 0);
         };
-        u32x4 fb[3][3][CNT], fa[3];   // ring of 3 steps: the weights of step s+2 load during step s
+        u32x4 fb[3][3][NB], fa[2][3];   // ring of 3 steps: the weights of step s+2 load during step s
         load_b(0, fb[0]);
         load_b(1, fb[1]);
 #pragma unroll
         for (int s = 0; s < 12; ++s) {
           if (s + 2 < 12) load_b(s + 2, fb[(s + 2) % 3]);
-          if (s > 0 && (s & 1) == 0)   // chunk start: the running sum changes sign with the chunk's parts
+          if (s > 0 && (s & 1) == 0) {   // chunk start: the running sum changes sign with the chunk's parts
+            acc[0] = -acc[0];
+            acc[1] = -acc[1];
+            if constexpr (EX) accx = -accx;
+          }
 #pragma unroll
-            for (int i = 0; i < CNT; ++i) acc[i] = -acc[i];
+          for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-          for (int p = 0; p < 3; ++p) fa[p] = *(const u32x4*)(arow + p * WB_PLANE + s * 32);
+            for (int p = 0; p < 3; ++p)
+              fa[tt][p] = *(const u32x4*)(xp + p * WB_PLANE + (32 * tt + lr) * (WB_XS * 2) + lh * 16 + s * 32);
 #pragma unroll
-          for (int pr = SM::NPROD - 1; pr >= 0; --pr)   // smallest products first
+          for (int pr = SM::NPROD - 1; pr >= 0; --pr) {   // smallest products first
 #pragma unroll
-            for (int i = 0; i < CNT; ++i) acc[i] = mfma_k16<bf16_t>(fa[SM::PA[pr]], fb[s % 3][SM::PB[pr]][i], acc[i]);
+            for (int tt = 0; tt < 2; ++tt) acc[tt] = mfma_k16<bf16_t>(fa[tt][SM::PA[pr]], fb[s % 3][SM::PB[pr]][0], acc[tt]);
+            if constexpr (EX)
+              accx = mfma_k16<bf16_t>(tx ? fa[1][SM::PA[pr]] : fa[0][SM::PA[pr]], fb[s % 3][SM::PB[pr]][NB - 1], accx);
+          }
         }
         // six chunks (even): the running sum is -(x w); out = -acc + bias, to the group's q / k / v buffer
-#pragma unroll
-        for (int i = 0; i < CNT; ++i) {
-          const int col = 32 * sub[i] + lr;
-          const float bias = a.qkv_bias[which[i] * WB_C + 96 * g + col];
-          float* dst = qkv + which[i] * (WB_T * WB_QS) + col;
+        auto store = [&](const floatx16& c, int wh, int sb, int mt) {
+          const int col = 32 * sb + lr;
+          const float bias = a.qkv_bias[wh * WB_C + 96 * g + col];
+          float* dst = qkv + wh * (WB_T * WB_QS) + col;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int t = 32 * mt + 8 * (r >> 2) + 4 * lh + (r & 3);
-            dst[t * WB_QS] = -acc[i][r] + bias;
+            dst[t * WB_QS] = -c[r] + bias;
           }
-        }
+        };
+        store(acc[0], which[0], sub[0], 0);
+        store(acc[1], which[0], sub[0], 1);
+        if constexpr (EX) store(accx, which[NB - 1], sub[NB - 1], tx);
       };
-      if (wq < 2) gemm(std::integral_constant<int, 3>{});
-      else gemm(std::integral_constant<int, 2>{});
+      if (ex) gemm(std::true_type{});
+      else gemm(std::false_type{});
+      W6T(t3);
       for (int k = tid; k < 4 * 225; k += 512) {
         const int hl = k / 225, e = k - hl * 225;
         tab[k] = a.table[e * a.tab_sr + (4 * g + hl) * a.tab_sh];
@@ -168,6 +209,7 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
       __syncthreads();
       // the next window's activations: loaded now, consumed by its phase A (phase C issues no loads)
       if (g == 1 && win + (int)gridDim.x < nwin) load_x(win + gridDim.x);
+      W6T(t4);
 
       // ---- phase C: attention of the group's 4 heads, wave = (head, query tile); the unfused kernel's
       // per-tile arithmetic (attention_mfma.hip, SPLIT) with q / k / v read from LDS
@@ -211,6 +253,7 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
 #pragma unroll
             for (int tj = 0; tj < 2; ++tj) S[tj] = mfma_k16<bf16_t>(kp[tj][SM::PA[pr]], qp[SM::PB[pr]], S[tj]);
         }
+        W6T(t5);
         // bias + mask + softmax over the keys of query i (lane column); key j of register r of tile tj:
         // j = 32 tj + 8 (r >> 2) + 4 h + (r & 3)
         const int split = WB_WS - a.shift;
@@ -266,6 +309,7 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
 #pragma unroll
           for (int r = 0; r < 16; ++r) S[tj][r] *= inv;
 
+        W6T(t6);
         // O^T[c][i] = sum_j V^T[c][j] P^T[j][i]: lane (c = lr, half lh) reads V^T row c in the permuted
         // key order of P's registers (keys j0 .. j0+3 and j0+8 .. j0+11)
         floatx16 O;
@@ -301,6 +345,11 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
           }
         }
       }
+      W6T(t7);
+#if W6_STAMP
+      s_b0 += t2 - (g == 0 ? t1 : te); s_gemm += t3 - t2; s_b1 += t4 - t3; s_s += t5 - t4; s_sm += t6 - t5; s_pv += t7 - t6;
+      te = t7;
+#endif
     }
     __syncthreads();   // every wave past this window's phase C (and its qkv GEMMs: the planes are free)
     if constexpr (PROJ) {
@@ -390,7 +439,20 @@ __global__ __launch_bounds__(512, 1) void wba_qkv_attn_kernel(const lic_wba_args
       else proj(std::integral_constant<int, 1>{});
     }
     __syncthreads();   // every wave done with this window before the next window's planes / qkv
+#if W6_STAMP
+    {
+      unsigned long long tz = 0;
+      W6T(tz);
+      s_be += tz - te;
+    }
+#endif
   }
+#if W6_STAMP
+  if (tid == 0) {
+    unsigned long long* o = (unsigned long long*)(a.out + (size_t)a.n * a.h * a.w * a.ldo) + (size_t)blockIdx.x * 8;
+    o[0] = s_a; o[1] = s_b0; o[2] = s_gemm; o[3] = s_b1; o[4] = s_s; o[5] = s_sm; o[6] = s_pv; o[7] = s_be;
+  }
+#endif
 }
 
 }  // namespace lic
