@@ -371,6 +371,22 @@ typedef struct lic_wgrad_args {
 int64_t lic_conv2d_wgrad_workspace(const lic_wgrad_args* a);   /* bytes, -1 on bad args */
 int lic_conv2d_wgrad(const lic_wgrad_args* a, lic_stream_t stream);
 
+/* Deferred split-K reduce (a training step's weight gradients summed by ONE launch after the
+ * backward; round 6).  lic_conv2d_wgrad_partials: when the tiled 16-bit kernel applies, launches
+ * only its partial sums into a->ws and sets *nsplit (> 0): dw / db are NOT written until a
+ * lic_wgrad_reduce_batch over a descriptor of this call runs; otherwise runs lic_conv2d_wgrad
+ * whole and sets *nsplit = 0.  lic_wgrad_reduce_blocks(a): the call's 256-thread reduce blocks.
+ * lic_wgrad_reduce_batch: `desc` is DEVICE memory holding n descriptors of
+ * LIC_WGRAD_RED_DESC_WORDS int64 each,
+ *   { ws, wsb (bias partials = ws + nsplit*ntaps*co*ci floats, or 0), dw, db (or 0), s_co, s_ci,
+ *     s_tap, nsplit, ntaps, co, ci, co_out, ci_out, accumulate, first_block, 0 },
+ * ascending first_block; the per-element sums are lic_conv2d_wgrad's (same order: bit-identical).
+ * Replaces the per-layer reduce of train_net_unet.py:177-200's loss.backward(). */
+#define LIC_WGRAD_RED_DESC_WORDS 16
+int lic_conv2d_wgrad_partials(const lic_wgrad_args* a, int32_t* nsplit, lic_stream_t stream);
+int32_t lic_wgrad_reduce_blocks(const lic_wgrad_args* a);
+int lic_wgrad_reduce_batch(const int64_t* desc, int32_t n, int32_t nblocks, lic_stream_t stream);
+
 /* Per-channel sum over pixels (bias / beta gradients): out[c] (+)= sum_p x[p*ldx + c].
  * fp32 out; workspace lic_channel_sum_workspace(c) bytes.                          */
 int64_t lic_channel_sum_workspace(int32_t c);

@@ -53,7 +53,9 @@ EXPORTED_SYMBOLS = (
     "lic_recon_train_fwd", "lic_recon_train_bwd", "lic_dwconv_wgrad_workspace", "lic_dwconv_wgrad",
     "lic_resunit_fwd", "lic_patches", "lic_wba_qkv_attn_fwd", "lic_wba16_qkv_attn_fwd", "lic_pack_taps",
     "lic_pack_taps_batch", "lic_pack_block_elems", "lic_rb3_chain_fwd",
+    "lic_conv2d_wgrad_partials", "lic_wgrad_reduce_blocks", "lic_wgrad_reduce_batch",
 )
+WGRAD_RED_DESC_WORDS = 16   # include/lic.h LIC_WGRAD_RED_DESC_WORDS
 LIC_EB_PARAMS = 58
 
 
@@ -246,6 +248,8 @@ def load():
         "lic_csam_fwd": [I, V, I, I, I, I, I, V, V, I, V],
         "lic_recon_fwd": [I, V, I, I, I, I, I, V, I, I, V, V, V, V, I, V, I, I, V],
         "lic_conv2d_wgrad": [V, V],
+        "lic_conv2d_wgrad_partials": [V, V, V],
+        "lic_wgrad_reduce_batch": [V, I, I, V],
         "lic_channel_sum": [I, V, I, I, I, V, L, V, I, V],
         "lic_act_fwd": [I, V, I, I, I, I, F, V, I, V],
         "lic_act_bwd": [I, V, I, V, I, I, I, I, F, V, I, V],
@@ -285,7 +289,8 @@ def load():
                        ("lic_dwconv_wgrad_workspace", [I, I, I, I, I])):
         getattr(lib, name).argtypes = argt
         getattr(lib, name).restype = ctypes.c_int64
-    for name, argt in (("lic_rate_train_parts", [I, I]), ("lic_recon_train_blocks", [I])):
+    for name, argt in (("lic_rate_train_parts", [I, I]), ("lic_recon_train_blocks", [I]),
+                       ("lic_wgrad_reduce_blocks", [V])):
         getattr(lib, name).argtypes = argt
         getattr(lib, name).restype = ctypes.c_int32
     lib.lic_last_error.restype = ctypes.c_char_p

@@ -31,7 +31,7 @@ from . import functional as Fn
 from ._ffi import ACT_NONE, EPI_GDN_DIV, EPI_GDN_RSQRT, EPI_GDN_SQRT, PRO_NONE, PRO_SQUARE, AttnArgs, WgradArgs, check
 from .functional import Act, ConvPack, _dp, dtype_id, stream_handle
 
-__all__ = ["conv2d", "conv_transpose2d", "gdn", "activation", "wgrad", "channel_sum", "dgrad_packs"]
+__all__ = ["conv2d", "conv_transpose2d", "gdn", "activation", "wgrad", "channel_sum", "dgrad_packs", "WgradDefer"]
 
 
 def _lib():
@@ -59,14 +59,95 @@ def _taps(kh, kw, pt, pl):
     return [ky - pt for ky in range(kh) for kx in range(kw)], [kx - pl for ky in range(kh) for kx in range(kw)]
 
 
+# --------------------------------------------------------------------------- deferred wgrad reduce
+class WgradDefer:
+    """The split-K reduces of a backward's weight gradients as ONE launch (lic_wgrad_reduce_batch)
+    instead of one per layer (~470 per bf16 training step).  Inside ``with defer:`` the conv /
+    transposed-conv backward launch only their wgrad partial sums (lic_conv2d_wgrad_partials) and
+    return dw / db that are written by ``flush()`` -- called on exit, before anything reads them
+    (train_net_unet.py: after ``loss.backward()``, before the gradient all-reduce / clip / Adam).
+    The per-element sums are the per-layer reduce's: bit-identical gradients
+    (tests/test_gpu_train.py::test_wgrad_defer_bit_identical).
+
+    Not for a backward whose gradient hooks read .grad during the backward (the eager multi-rank
+    GradAllReduce) or whose parameters receive several contributions (the engine would add unreduced
+    tensors): the training loop enables it for the one-GPU and captured steps, whose parameters each
+    feed one convolution.  Captured steps: the descriptor table is a device buffer sized by an eager
+    step; ``finalize()`` after the capture writes the captured call's descriptors into it."""
+    def __init__(self):
+        self.rows = []        # descriptors of this backward's deferred calls
+        self.keep = []        # their workspaces, alive until the reduce is launched
+        self.desc = None      # device table [capacity, WORDS] int64
+        self.pending = None   # captured rows, written by finalize()
+
+    def __enter__(self):
+        global _DEFER
+        if _DEFER is not None:
+            raise RuntimeError("WgradDefer: already active")
+        _DEFER = self
+        self.rows, self.keep = [], []
+        return self
+
+    def __exit__(self, *exc):
+        global _DEFER
+        _DEFER = None
+        if exc[0] is None:
+            self.flush()
+        self.rows, self.keep = [], []
+        return False
+
+    def add(self, a: WgradArgs, ws: torch.Tensor, nsplit: int) -> None:
+        nblk = int(_lib().lic_wgrad_reduce_blocks(ctypes.byref(a)))
+        first = self.rows[-1][14] + self.rows[-1][15] if self.rows else 0
+        wsb = (a.ws + nsplit * a.ntaps * a.co * a.ci * 4) if a.db else 0
+        # (word 15 holds the call's block count while recording; the table's word 15 is 0)
+        self.rows.append([a.ws, wsb, a.dw, a.db or 0, a.s_co, a.s_ci, a.s_tap, nsplit, a.ntaps, a.co, a.ci,
+                          a.co_out, a.ci_out, a.accumulate, first, nblk])
+        self.keep.append(ws)
+
+    def flush(self) -> None:
+        if not self.rows:
+            return
+        n = len(self.rows)
+        nblocks = self.rows[-1][14] + self.rows[-1][15]
+        if nblocks >= 2 ** 31:
+            raise ValueError("WgradDefer: more than 2^31 reduce blocks")
+        rows = [r[:15] + [0] for r in self.rows]
+        dev = self.keep[0].device
+        if torch.cuda.is_current_stream_capturing():
+            # no host-to-device copy inside a capture: the table buffer exists (sized by the eager
+            # warm-up step) and is filled by finalize() once the capture has ended
+            if self.desc is None or self.desc.shape[0] < n:
+                raise RuntimeError("WgradDefer: run one eager step with this object before capturing")
+            self.pending = rows
+        else:
+            t = torch.tensor(rows, dtype=torch.int64)
+            if self.desc is None or self.desc.shape[0] < n:
+                self.desc = torch.zeros((n, _ffi.WGRAD_RED_DESC_WORDS), dtype=torch.int64, device=dev)
+            self.desc[:n].copy_(t.to(dev))
+        check(_lib().lic_wgrad_reduce_batch(_dp(self.desc), n, int(nblocks), stream_handle()))
+
+    def finalize(self) -> None:
+        """After a capture: the captured step's descriptors into the table its reduce launch reads."""
+        if self.pending is not None:
+            torch.cuda.synchronize()
+            self.desc[:len(self.pending)].copy_(torch.tensor(self.pending, dtype=torch.int64).to(self.desc.device))
+            torch.cuda.synchronize()
+            self.pending = None
+
+
+_DEFER: Optional[WgradDefer] = None
+
+
 # --------------------------------------------------------------------------- primitives
 def wgrad(x: torch.Tensor, dz: torch.Tensor, dy: Sequence[int], dx: Sequence[int], *, stride: int = 1,
           lattice: Optional[Tuple[int, int]] = None, dw: torch.Tensor, strides: Tuple[int, int, int],
           co_out: int, ci_out: int, prologue: int = PRO_NONE, accumulate: bool = False,
-          db: Optional[torch.Tensor] = None) -> torch.Tensor:
+          db: Optional[torch.Tensor] = None, deferrable: bool = False) -> torch.Tensor:
     """dw[n*s_co + c*s_ci + t*s_tap] (+)= sum_pix dz[pix, n] * pro(x[pix*stride + tap_t, c]).
     x, dz: NHWC with 16-byte channel counts; lattice = (mi, mj) output pixels (default dz's map).
-    db (fp32 [co_out], optional): the bias gradient sum_pix dz[pix, n] from the same launch."""
+    db (fp32 [co_out], optional): the bias gradient sum_pix dz[pix, n] from the same launch.
+    deferrable: inside a WgradDefer, dw / db may be written by its flush (nothing reads them before)."""
     if x.dtype != dz.dtype:
         raise ValueError("wgrad: x and dz dtypes differ")
     if dw.dtype != torch.float32 or not dw.is_contiguous():
@@ -97,6 +178,12 @@ def wgrad(x: torch.Tensor, dz: torch.Tensor, dy: Sequence[int], dx: Sequence[int
         check(_lib().lic_conv2d_wgrad(ctypes.byref(a), stream_handle()))  # raises with the reason
     ws = torch.empty((max(need, 4) // 4,), dtype=torch.float32, device=x.device)
     a.ws, a.ws_bytes = _dp(ws), need
+    if deferrable and _DEFER is not None:
+        ns = ctypes.c_int32(0)
+        check(_lib().lic_conv2d_wgrad_partials(ctypes.byref(a), ctypes.byref(ns), stream_handle()))
+        if ns.value > 0:
+            _DEFER.add(a, ws, ns.value)
+        return dw
     check(_lib().lic_conv2d_wgrad(ctypes.byref(a), stream_handle()))
     return dw
 
@@ -219,7 +306,7 @@ class _Conv2dFn(torch.autograd.Function):
             # the bias gradient comes out of the same launch (column sums of the staged dz tiles)
             db = torch.empty((co,), dtype=torch.float32, device=dz.device) if want_db else None
             wgrad(xp, dzp, tdy, tdx, stride=stride, dw=dw, strides=(ci * kh * kw, kh * kw, 1), co_out=co,
-                  ci_out=ci, db=db)
+                  ci_out=ci, db=db, deferrable=weight.dtype == torch.float32)
             dw = dw.to(weight.dtype)
         if want_db and db is None:
             db = channel_sum(dz)
@@ -276,7 +363,7 @@ class _ConvT2dFn(torch.autograd.Function):
             dw = torch.empty((ci, co, kh, kw), dtype=torch.float32, device=dz.device)
             tdy, tdx = _taps(kh, kw, pt, pl)
             wgrad(dzp, xp, tdy, tdx, stride=s, lattice=(H, W), dw=dw, strides=(co * kh * kw, kh * kw, 1),
-                  co_out=ci, ci_out=co)
+                  co_out=ci, ci_out=co, deferrable=weight.dtype == torch.float32)
             dw = dw.to(weight.dtype)
         if has_bias and ctx.needs_input_grad[2]:
             db = channel_sum(dz)

@@ -1177,6 +1177,58 @@ static inline unsigned tr_nblk(int64_t total) { return (unsigned)((total + 255) 
 // wgrad_tr.hip: the tiled 16-bit kernel (all taps of a tap group per work-group, transpose reads)
 namespace lic {
 int wgrad_tr_nsplit(const lic_wgrad_args& a);
+// Many wgrad_reduce_kernel launches in one (lic_wgrad_reduce_batch): block b finds its descriptor by
+// binary search over the ascending first blocks and runs the same per-element sum (same order).
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(const int64_t* __restrict__ desc, int n) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[(int64_t)mid * LIC_WGRAD_RED_DESC_WORDS + 14] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t* d = desc + (int64_t)lo * LIC_WGRAD_RED_DESC_WORDS;
+  const int64_t idx = (int64_t)(b - (int)d[14]) * 256 + threadIdx.x;
+  const int ntaps = (int)d[8], co = (int)d[9], ci = (int)d[10], co_out = (int)d[11], ci_out = (int)d[12];
+  const int64_t total = (int64_t)ntaps * co_out * ci_out;
+  const float* wsb = (const float*)d[1];
+  float* db = (float*)d[3];
+  const int nsplit = (int)d[7], accumulate = (int)d[13];
+  if (idx >= total) {
+    const int nn = (int)(idx - total);
+    if (!wsb || nn >= co_out) return;
+    float b0 = 0.f, b1 = 0.f;
+    int k = 0;
+    for (; k + 2 <= nsplit; k += 2) {
+      b0 += wsb[(int64_t)k * co + nn];
+      b1 += wsb[(int64_t)(k + 1) * co + nn];
+    }
+    if (k < nsplit) b0 += wsb[(int64_t)k * co + nn];
+    db[nn] = accumulate ? db[nn] + (b0 + b1) : b0 + b1;
+    return;
+  }
+  const float* ws = (const float*)d[0];
+  float* dw = (float*)d[2];
+  const int c = (int)(idx % ci_out);
+  const int64_t r = idx / ci_out;
+  const int nn = (int)(r % co_out);
+  const int t = (int)(r / co_out);
+  const int64_t stride = (int64_t)ntaps * co * ci;
+  const float* p = ws + ((int64_t)t * co + nn) * ci + c;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= nsplit; k += 4) {
+    s0 += p[k * stride];
+    s1 += p[(k + 1) * stride];
+    s2 += p[(k + 2) * stride];
+    s3 += p[(k + 3) * stride];
+  }
+  for (; k < nsplit; ++k) s0 += p[k * stride];
+  const float sm = (s0 + s1) + (s2 + s3);
+  float* o = dw + nn * d[4] + c * d[5] + t * d[6];
+  *o = accumulate ? *o + sm : sm;
+}
+
 int wgrad_tr_launch(const lic_wgrad_args& a, hipStream_t s, int* nsplit);
 }  // namespace lic
 
@@ -1195,6 +1247,38 @@ static int64_t wgrad_ws_bytes(const lic_wgrad_args& a, int* nsplit_out, bool* ti
 extern "C" int64_t lic_conv2d_wgrad_workspace(const lic_wgrad_args* a) {
   if (!a || wgrad_check(*a)) return -1;
   return wgrad_ws_bytes(*a, nullptr, nullptr);
+}
+
+extern "C" int lic_conv2d_wgrad_partials(const lic_wgrad_args* ap, int32_t* nsplit_out, lic_stream_t stream) {
+  if (!ap || !nsplit_out) return fail("wgrad partials: null args");
+  const lic_wgrad_args& a = *ap;
+  if (int e = wgrad_check(a)) return e;
+  int nsplit = 0;
+  bool tiled = false;
+  const int64_t need = wgrad_ws_bytes(a, &nsplit, &tiled);
+  if (!tiled) {   // the generic kernel: the whole wgrad now, nothing left to defer
+    *nsplit_out = 0;
+    return lic_conv2d_wgrad(ap, stream);
+  }
+  if (!a.ws || a.ws_bytes < need)
+    return fail("wgrad partials: workspace too small (" + std::to_string(a.ws_bytes) + " < " + std::to_string(need) + ")");
+  int ns = 0;
+  if (int e = wgrad_tr_launch(a, (hipStream_t)stream, &ns)) return e;
+  *nsplit_out = ns;
+  return 0;
+}
+
+extern "C" int32_t lic_wgrad_reduce_blocks(const lic_wgrad_args* a) {
+  if (!a) return -1;
+  const int64_t total = (int64_t)a->ntaps * a->co_out * a->ci_out + (a->db ? a->co_out : 0);
+  return (int32_t)((total + 255) / 256);
+}
+
+extern "C" int lic_wgrad_reduce_batch(const int64_t* desc, int32_t n, int32_t nblocks, lic_stream_t stream) {
+  if (!desc || n <= 0 || nblocks <= 0) return fail("lic_wgrad_reduce_batch: need descriptors and blocks");
+  hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, desc, n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail(std::string("lic_wgrad_reduce_batch: ") + hipGetErrorString(e));
 }
 
 extern "C" int lic_conv2d_wgrad(const lic_wgrad_args* ap, lic_stream_t stream) {

@@ -5,6 +5,8 @@ the same seeded inputs and upstream gradients.
 Tolerances: fp32 path — relative 1e-4 of each gradient's max magnitude (the MFMA
 wgrad sums ~1e3-1e5 products per element in a different order than oneDNN);
 fp16 path — 2e-2 of the max magnitude (fp16 operands, fp32 accumulation)."""
+import contextlib
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -365,3 +367,54 @@ def test_recon_mse_grad(dtype):
         return ((xt - img) ** 2).mean()
 
     _check(lambda x_, w_: AG.recon_mse(x_, w_, img.to(DEV)), ref, [x16, cw], [True, True], dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_wgrad_defer_bit_identical(dtype):
+    """autograd.WgradDefer (the split-K wgrad reduces of a backward as one lic_wgrad_reduce_batch
+    launch after it) gives the same dw / db / dx bits as the per-layer reduce: a 3x3 (bias, GELU),
+    a 1x1, a stride-2 3x3, a 5x5 s2 ZeroPad conv and a transposed conv, eagerly and replayed from a
+    hipGraph capture (the table filled by finalize())."""
+    from lic_amd import autograd as AG
+    from lic_amd._ffi import ACT_GELU
+    torch.manual_seed(5)
+    x0 = torch.randn(2, 32, 32, 64, device=DEV).to(dtype)
+    ws = [torch.randn(64, 64, 3, 3, device=DEV) * 0.05, torch.randn(96, 64, 1, 1, device=DEV) * 0.1,
+          torch.randn(64, 96, 3, 3, device=DEV) * 0.05, torch.randn(64, 64, 5, 5, device=DEV) * 0.03,
+          torch.randn(64, 32, 5, 5, device=DEV) * 0.03]
+    bs = [torch.randn(w.shape[0] if i != 4 else 32, device=DEV) * 0.1 for i, w in enumerate(ws)]
+    dy = torch.randn(2, 16, 16, 32, device=DEV).to(dtype)
+
+    def step(defer):
+        x = x0.clone().requires_grad_(True)
+        ps = [t.clone().requires_grad_(True) for t in ws + bs]
+        w, b = ps[:5], ps[5:]
+        h = AG.conv2d(x, w[0], b[0], 1, 1, ACT_GELU)
+        h = AG.conv2d(h, w[1], b[1], 1, 0)
+        h = AG.conv2d(h, w[2], b[2], 2, 1)
+        h = AG.conv2d(h, w[3], b[3], 1, (1, 1, 2, 2))[:, :8, :8].contiguous()
+        y = AG.conv_transpose2d(h, w[4], b[4], 2, 3, 1, (1, 1))
+        with defer if defer is not None else contextlib.nullcontext():
+            y.backward(dy[:, :y.shape[1], :y.shape[2]].contiguous())
+        return [x.grad] + [p.grad for p in ps]
+
+    ref = step(None)
+    d = AG.WgradDefer()
+    got = step(d)
+    torch.cuda.synchronize()
+    for i, (r, g) in enumerate(zip(ref, got)):
+        assert torch.equal(r, g), f"gradient {i} differs with the deferred reduce"
+    # captured: the table is sized by the eager run above, filled after the capture
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        step(d)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, stream=s):
+            outs = step(d)
+    d.finalize()
+    graph.replay()
+    torch.cuda.synchronize()
+    for i, (r, g) in enumerate(zip(ref, outs)):
+        assert torch.equal(r, g), f"gradient {i} differs in the captured deferred step"

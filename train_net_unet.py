@@ -89,6 +89,9 @@ def main():
                          "one hipGraph and replay it: no per-launch host cost; the noise seed lives on the device "
                          "(bf16 / fp32, any world size; the default there)")
     ap.add_argument("--eager", action="store_true", help="run every step eagerly (no hipGraph capture)")
+    ap.add_argument("--ref-clip", action="store_true",
+                    help="the reference's exact clip: gradients of every parameter (the non-optimised slice "
+                         "modules' accumulating across steps) in clip_grad_norm_ (train_net_unet.py:198)")
     args = ap.parse_args()
 
     from lic_amd import distributed as D
@@ -97,6 +100,7 @@ def main():
         sys.exit(D.launch_workers([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
     from lic_amd.model import net_ga, net_unet_ha_hs
     from lic_amd import functional as Fn
+    from lic_amd import autograd as AG
     rank, world, local = D.init("nccl")
     if D.launched() and args.gpus > 1 and world != args.gpus:
         raise SystemExit(f"train_net_unet.py: --gpus {args.gpus} but the launcher started {world} ranks")
@@ -118,6 +122,17 @@ def main():
         net.load_state_dict(torch.load(args.weight_path, map_location="cpu", weights_only=True), strict=True)
     net = net.to(dev)
     params = net.base_params()
+    # The reference optimises base_params() only (train_net_unet.py:132) and its opt.zero_grad() clears
+    # only theirs: the slice-loop modules (atten_mean / atten_scale, cc_*_transforms, lrp_transforms) are
+    # never updated, their .grad only grows, and :198 clips over ALL net.parameters(), growing norms
+    # included.  Default here: those modules take no weight gradient at all (requires_grad off: no
+    # wgrad launches, no AccumulateGrad additions -- ~300 per step) and the clip runs over the
+    # optimised parameters; --ref-clip keeps the reference's accumulate-and-clip-over-everything.
+    if not args.ref_clip:
+        opt_ids = {id(p) for p in params}
+        for p in net.parameters():
+            if id(p) not in opt_ids:
+                p.requires_grad_(False)
     if args.graph and args.precision == "fp16":
         raise SystemExit("--graph: bf16 / fp32 (fp16's GradScaler syncs the host every step)")
     # capturable Adam keeps lr and the step count on the device (graph replays update them); fused:
@@ -127,6 +142,16 @@ def main():
                            capturable=args.graph, fused=os.environ.get("LIC_FUSED_ADAM", "1") != "0")
     sch = torch.optim.lr_scheduler.MultiStepLR(opt, [1500, 2500, 3500, 4000], 0.5)
     sync = D.GradAllReduce(params, world)
+    # one GPU: the backward's split-K wgrad reduces as one launch after it (autograd.WgradDefer; at
+    # world > 1 the eager GradAllReduce hooks read .grad during the backward).  LIC_WGRAD_DEFER=0: off
+    # (--ref-clip: the accumulating gradients would be added before their reduce ran)
+    wdefer = AG.WgradDefer() if (world == 1 and not args.ref_clip and
+                                 os.environ.get("LIC_WGRAD_DEFER", "1") != "0") else None
+    clip_params = list(net.parameters()) if args.ref_clip else params
+
+    def backward(t):
+        with wdefer if wdefer is not None else contextlib.nullcontext():
+            t.backward()
     scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 10, enabled=args.precision == "fp16")
     batches = Crops(synthetic_bank(16, 2 * args.crop, 5000 + 97 * rank, dev), B, args.crop, 1234 + rank)
 
@@ -135,7 +160,7 @@ def main():
     def step_body(x, seed_dev=None):
         bpp, mse = net(x, "train", seed_dev=seed_dev)
         loss = args.lmbda * 255 ** 2 * mse + bpp                       # :180
-        loss.backward()
+        backward(loss)
         sync.finish()                                                  # RCCL all-reduce, captured too
         torch.nn.utils.clip_grad_norm_(grad_params, 1.0)               # :198
         opt.step()
@@ -156,9 +181,9 @@ def main():
                 opt.zero_grad(set_to_none=True)
                 with plan.record() if (plan is not None and k == nwarm - 1) else contextlib.nullcontext():
                     bpp, mse = net(static_x, "train", seed_dev=seed_t)
-                    (args.lmbda * 255 ** 2 * mse + bpp).backward()
+                    backward(args.lmbda * 255 ** 2 * mse + bpp)
                 sync.finish()              # first collectives eagerly: communicator set up before capture
-                grad_params = [p for p in params if p.grad is not None]
+                grad_params = [p for p in clip_params if p.grad is not None]
                 torch.nn.utils.clip_grad_norm_(grad_params, 1.0)
                 opt.step()
                 seed_t.add_(1)
@@ -177,6 +202,8 @@ def main():
             with plan.replay() if plan is not None else contextlib.nullcontext():
                 outs = step_body(static_x, seed_t)
             seed_t.add_(1)
+        if wdefer is not None:
+            wdefer.finalize()
 
         def step():
             static_x.copy_(batches())
@@ -191,10 +218,10 @@ def main():
         opt.zero_grad(set_to_none=True)
         bpp, mse = net(x, "train")
         loss = args.lmbda * 255 ** 2 * mse + bpp                       # :180
-        scaler.scale(loss).backward()
+        backward(scaler.scale(loss))
         sync.finish()
         scaler.unscale_(opt)
-        torch.nn.utils.clip_grad_norm_([p for p in params if p.grad is not None], 1.0)   # :198
+        torch.nn.utils.clip_grad_norm_([p for p in clip_params if p.grad is not None], 1.0)   # :198
         scaler.step(opt)
         scaler.update()
         return loss.detach(), bpp.detach(), mse.detach()
