@@ -275,26 +275,49 @@ def _conv_dgrad(dzp: torch.Tensor, weight: torch.Tensor, stride: int, pad, H: in
 
 
 # --------------------------------------------------------------------------- Conv2d
+# activations whose derivative is a function of the output's sign (slope > 0): the conv applies them in
+# its epilogue and the backward reads the saved output -- no separate forward activation launch
+_SIGN_ACTS = (_ffi.ACT_RELU, _ffi.ACT_LRELU)
+
+
 class _Conv2dFn(torch.autograd.Function):
+    """y = act(conv(x) + b) [+ residual], or with res_act y = act(conv(x) + b + residual) (the conv's
+    RES_ACT epilogue).  The residual add is the conv epilogue's r1 operand (one rounding instead of
+    two launches); ReLU / LeakyReLU are epilogue activations whose backward reads the output's sign;
+    other activations (GELU) keep the pre-activation z for their backward."""
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, act, slope):
+    def forward(ctx, x, weight, bias, stride, pad, act, slope, residual, res_act):
         co, ci, kh, kw = weight.shape
         if x.shape[-1] != ci:
             raise ValueError(f"conv2d: input has {x.shape[-1]} channels, weight expects {ci}")
         xp = _pad_channels(x)
         pk = Fn.pack_conv2d(weight, bias, stride, pad, x.dtype, cin_to=xp.shape[-1])
-        z = Fn.conv(Act(xp), pk).t
-        y = _act_fwd(z, act, slope) if act != ACT_NONE else z
-        ctx.save_for_backward(xp, weight, z if act != ACT_NONE else None)
-        ctx.geom = (stride, tuple(pad), act, slope, x.shape[1], x.shape[2], bias is not None)
+        r1 = Act(residual.contiguous()) if residual is not None else None
+        if residual is not None and act != ACT_NONE and not res_act:
+            raise ValueError("conv2d: an activation before the residual add is not fused (act(conv) + r)")
+        if act in _SIGN_ACTS and slope > 0:
+            y = Fn.conv(Act(xp), pk, act=act, slope=slope, r1=r1,
+                        epi=_ffi.EPI_RES_ACT if r1 is not None else _ffi.EPI_PLAIN).t
+            saved, mode = y, 1
+        elif act != ACT_NONE:
+            z = Fn.conv(Act(xp), pk, r1=r1).t
+            y = _act_fwd(z, act, slope)
+            saved, mode = z, 2
+        else:
+            y = Fn.conv(Act(xp), pk, r1=r1).t
+            saved, mode = None, 0
+        ctx.save_for_backward(xp, weight, saved)
+        ctx.geom = (stride, tuple(pad), act, slope, x.shape[1], x.shape[2], bias is not None, mode)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         xp, weight, z = ctx.saved_tensors
-        stride, pad, act, slope, H, W, has_bias = ctx.geom
+        stride, pad, act, slope, H, W, has_bias, mode = ctx.geom
         co, ci, kh, kw = weight.shape
-        dz = _act_bwd(z, dy, act, slope) if act != ACT_NONE else dy.contiguous()
+        # mode 1: z is the output (act' from its sign); 2: the pre-activation
+        dz = _act_bwd(z, dy, act, slope) if mode else dy.contiguous()
+        dr = dz if ctx.needs_input_grad[7] else None   # the residual sees what the conv output sees
         dzp = _pad_channels(dz)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -310,16 +333,19 @@ class _Conv2dFn(torch.autograd.Function):
             dw = dw.to(weight.dtype)
         if want_db and db is None:
             db = channel_sum(dz)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, dr, None
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
-           pad=0, act: int = ACT_NONE, slope: float = 0.01) -> torch.Tensor:
+           pad=0, act: int = ACT_NONE, slope: float = 0.01, residual: Optional[torch.Tensor] = None,
+           res_act: bool = False) -> torch.Tensor:
     """act(F.conv2d(x, weight, bias, stride, padding)) on NHWC; pad = int or (top, left, bottom, right)
-    (asymmetric: nn.ZeroPad2d((l, r, t, b)) followed by a padding-0 conv)."""
+    (asymmetric: nn.ZeroPad2d((l, r, t, b)) followed by a padding-0 conv).  residual: + residual after
+    the conv (no activation), or with res_act act(conv + residual) -- one launch."""
     if isinstance(pad, int):
         pad = (pad, pad, pad, pad)
-    return _Conv2dFn.apply(x, weight, bias, int(stride), tuple(pad), int(act), float(slope))
+    return _Conv2dFn.apply(x, weight, bias, int(stride), tuple(pad), int(act), float(slope), residual,
+                           bool(res_act))
 
 
 # --------------------------------------------------------------------------- ConvTranspose2d

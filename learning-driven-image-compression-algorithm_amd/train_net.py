@@ -39,21 +39,24 @@ __all__ = ["net_forward_train", "analysis", "synthesis", "syntax", "generator", 
 
 
 # --------------------------------------------------------------------------- leaf layers
-def conv(m, x, act: int = ACT_NONE, slope: float = 0.01, pad=None):
+def conv(m, x, act: int = ACT_NONE, slope: float = 0.01, pad=None, residual=None, res_act: bool = False):
     """nn.Conv2d (reference names) on an NHWC tensor; pad overrides the symmetric padding
-    (top, left, bottom, right) for the ZeroPad2d + conv pairs."""
+    (top, left, bottom, right) for the ZeroPad2d + conv pairs.  residual: conv(x) + residual (res_act:
+    act(conv(x) + residual)) in the conv's epilogue."""
     if pad is None:
         p = m.padding[0]
         pad = (p, p, p, p)
     if m.groups != 1:
         y = AG.dwconv2d(x, m.weight, m.bias, m.stride[0], pad)
+        if residual is not None:
+            raise ValueError("conv: no fused residual for depthwise convs")
         return AG.activation(y, act, slope) if act != ACT_NONE else y
-    return AG.conv2d(x, m.weight, m.bias, m.stride[0], pad, act, slope)
+    return AG.conv2d(x, m.weight, m.bias, m.stride[0], pad, act, slope, residual=residual, res_act=res_act)
 
 
-def linear(m, x, act: int = ACT_NONE, slope: float = 0.01):
-    """nn.Linear over the channels of every pixel (a 1x1 convolution)."""
-    return AG.conv2d(x, m.weight[:, :, None, None], m.bias, 1, 0, act, slope)
+def linear(m, x, act: int = ACT_NONE, slope: float = 0.01, residual=None):
+    """nn.Linear over the channels of every pixel (a 1x1 convolution); + residual in its epilogue."""
+    return AG.conv2d(x, m.weight[:, :, None, None], m.bias, 1, 0, act, slope, residual=residual)
 
 
 def conv_t(m, x, prepad=(1, 1)):
@@ -82,7 +85,7 @@ def residual_bottleneck(m, x):
     b = m.branch
     t = conv(b[0], x, ACT_GELU)
     t = conv(b[2], t, ACT_GELU)
-    return AG.add(conv(b[4], t), x)
+    return conv(b[4], t, residual=x)
 
 
 def residual_block(m, x):
@@ -106,7 +109,7 @@ def residual_unit(m, x):
     c = m.conv
     t = conv(c[0], x, ACT_RELU)
     t = conv(c[2], t, ACT_RELU)
-    return AG.activation(AG.add(conv(c[4], t), x), ACT_RELU)
+    return conv(c[4], t, ACT_RELU, residual=x, res_act=True)
 
 
 def wba(m, x):
@@ -116,7 +119,7 @@ def wba(m, x):
     a = AG.win_attn(qkv, at.relative_position_bias_table, m.dim, m.num_heads, m.window_size, m.shift_size,
                     tab_sr=m.num_heads, tab_sh=1, mask_kind=1 if m.shift_size > 0 else 0, scale_after=False,
                     scale=float(at.scale))
-    return AG.add(linear(at.proj, a), x)
+    return linear(at.proj, a, residual=x)
 
 
 def win_noshift_attention(m, x):
@@ -146,7 +149,7 @@ def wmsa(m, x, residual):
     table = m.relative_position_params.contiguous()   # [heads, 2ws-1, 2ws-1]
     a = AG.win_attn(qkv, table, m.input_dim, m.n_heads, ws, ws // 2 if sw else 0, tab_sr=1,
                     tab_sh=(2 * ws - 1) ** 2, mask_kind=2 if sw else 0, scale_after=True, scale=float(m.scale))
-    return AG.add(linear(m.linear, a), residual)
+    return linear(m.linear, a, residual=residual)
 
 
 def block_1(m, x):
@@ -155,7 +158,7 @@ def block_1(m, x):
     x1 = wmsa(m.msa, y, x)
     y = AG.layernorm(x1, m.ln2.weight, m.ln2.bias, m.ln2.eps)
     h = linear(m.mlp[0], y, ACT_GELU)
-    return AG.add(linear(m.mlp[2], h), x1)
+    return linear(m.mlp[2], h, residual=x1)
 
 
 def swin_block(m, x):
@@ -278,11 +281,11 @@ def unet_ha_new(m, x):
     C = x.shape[-1]
     h = C // 2
     cat1 = torch.cat([residual_block3_5(m.conv1, _c(x[..., h:])), wba(m.SpatialTransformer1, _c(x[..., :h]))], -1)
-    d = AG.add(conv(m.down0, cat1), x)
+    d = conv(m.down0, cat1, residual=x)
     down_x1 = conv(m.down1, d, ACT_GELU)
     cat2 = torch.cat([residual_block5x5(m.conv2, _c(down_x1[..., :128])),
                       wba(m.SpatialTransformer2, _c(down_x1[..., 128:]))], -1)
-    d2 = conv(m.down2, AG.add(conv(m.down3, cat2), down_x1), ACT_GELU)
+    d2 = conv(m.down2, conv(m.down3, cat2, residual=down_x1), ACT_GELU)
     mm = residual_bottleneck(m.middle[0], d2)
     mm = wba(m.middle[1], mm)
     mm = residual_bottleneck(m.middle[2], mm)
@@ -293,11 +296,11 @@ def unet_hs_new(m, middle_x, down_x1, inp):
     """Unet_hs_new.forward (Block_unet.py:868-890); its first argument (z_hat) is never read."""
     cat0 = torch.cat([residual_block3x3(m.conv3, _c(middle_x[..., 256:])),
                       wba(m.SpatialTransformer3, _c(middle_x[..., :256]))], -1)
-    u = AG.add(conv(m.up0, cat0), middle_x)
+    u = conv(m.up0, cat0, residual=middle_x)
     u1 = conv_t1(m.up3, torch.cat([conv_t1(m.up1, u, ACT_GELU), down_x1], -1), ACT_GELU)
     cat2 = torch.cat([residual_block3x3(m.conv4, _c(u1[..., :128])), wba(m.SpatialTransformer2, _c(u1[..., 128:]))],
                      -1)
-    u2 = AG.add(conv(m.up5, cat2), u1)
+    u2 = conv(m.up5, cat2, residual=u1)
     u2 = conv_t1(m.up2, u2, ACT_GELU)
     return conv_t1(m.up4, torch.cat([u2, inp], -1))
 

@@ -68,6 +68,25 @@ def _run(fn_gpu, fn_ref, x, params, dtype, seed=3):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("act,res_act", [("none", False), ("relu", True), ("lrelu", True), ("gelu", True)])
+def test_conv2d_residual_grad(dtype, act, res_act):
+    """conv2d(..., residual=r): conv + r in the conv epilogue (residual_bottleneck, the proj / MLP
+    Linears, the U-Net skips), res_act: act(conv + r) (compressai ResidualUnit's relu(conv + x)); the
+    residual's gradient is the conv output's."""
+    from lic_amd import autograd as AG
+    from lic_amd._ffi import ACT_GELU, ACT_LRELU, ACT_NONE, ACT_RELU
+    code = {"none": ACT_NONE, "gelu": ACT_GELU, "lrelu": ACT_LRELU, "relu": ACT_RELU}[act]
+    ref_act = {"none": lambda v: v, "gelu": F.gelu, "lrelu": lambda v: F.leaky_relu(v, 0.01), "relu": F.relu}[act]
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 32, 12, 12, generator=g)
+    w = torch.randn(48, 32, 3, 3, generator=g) / (32 * 9) ** 0.5
+    b = torch.randn(48, generator=g) * 0.1
+    r = torch.randn(2, 48, 12, 12, generator=g)
+    _run(lambda xg, wg, bg, rg: AG.conv2d(xg, wg, bg, 1, 1, code, residual=_nhwc(rg).to(xg.dtype), res_act=res_act),
+         lambda xr, wr, br, rr: ref_act(F.conv2d(xr, wr, br, 1, 1) + rr), x, [w, b, r], dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("ci,co,k,s,pad", [
     (64, 64, 3, 1, 1),     # RB / WNSA conv3x3
     (192, 192, 3, 1, 1),   # full-width 3x3 (128-wide wgrad tiles)
