@@ -41,9 +41,7 @@ static int conv_halo_dispatch(const lic_conv_args& a, hipStream_t s, int& status
     if (a.ntaps == 1 || a.ci <= 16) {
       if (int r = gemm16_dispatch<T>(a, s, status)) return r;
     }
-    if (a.ntaps > 1) {
-      if (int r = conv16_dispatch<T>(a, s, status)) return r;
-    }
+    if (int r = conv16_dispatch<T>(a, s, status)) return r;   // (1x1: small maps only)
   }
   const bool gemm_ok = a.ntaps == 1 && (HALO_1X1 == 2 || (HALO_1X1 == 1 && sizeof(T) == 4));
   if (a.groups != 1 || (a.ntaps < 2 && !gemm_ok) || a.prologue != LIC_PRO_NONE || a.force_direct) return 0;

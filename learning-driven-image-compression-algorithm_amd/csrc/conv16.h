@@ -593,6 +593,18 @@ int conv16_dispatch_impl(const lic_conv_args& a, hipStream_t s, int& status) {
   if (!on || a.force_mfma_generic || a.force_direct) return 0;
   auto blocks = [&](int bn) { return (int64_t)a.n * ((a.mi + 15) / 16) * ((a.mj + 31) / 32) * (a.copad / bn); };
   const bool big = a.mi >= 16 && a.mj >= 32 && small_on != 2;
+  // 1x1 on small maps (after gemm16 declined: K not 96 / 192 or < 4 K pixels), e.g. the slice loop's
+  // 128-channel Linears at 16x16: 4 x 16-pixel tiles x 32 channels, K split over the 4 waves, instead of
+  // the generic kernel's 64-pixel x 128-channel tiles (32 workgroups at 2 K pixels).  A/B: LIC_CONV16S_1X1=0
+  if (a.ntaps == 1) {
+    static const int on1 = wd_env("LIC_CONV16S_1X1", 1);
+    if (!on1 || !small_on || a.isy != 1 || a.isx != 1 || a.dy[0] != 0 || a.dx[0] != 0 || a.copad % 32 ||
+        (int64_t)a.n * a.mi * a.mj > 8192)
+      return 0;
+    const int64_t sb1 = (int64_t)a.n * ((a.mi + 3) / 4) * ((a.mj + 15) / 16) * (a.copad / 32);
+    if (sb1 > 2048 && a.copad % 64 == 0 && try_conv16s<T, 1, 1, 2>(a, s, status)) return 1;
+    return try_conv16s<T, 1, 1, 1>(a, s, status);
+  }
   if (a.isy == 1 && a.isx == 1) {
     if (a.ntaps == 9 && big) {
       if (a.copad % 192 == 0 && blocks(192) >= 128) return try_conv16<T, 3, 3, 1, 9, 192, 2>(a, s, status);

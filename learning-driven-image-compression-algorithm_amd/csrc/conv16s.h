@@ -73,7 +73,8 @@ struct C16sGeo {
   static constexpr int RED = NW * NQ * TILE * 4;    // the waves' partial tiles
   // weight ring: R slots (R divides the tap count, so a chunk starts at slot 0), prefetch distance R - 1:
   // (a 9-deep ring for 3x3 -- a whole chunk ahead -- was slower: 19.0 -> 22.9 us at 16x16, r05n)
-  static constexpr int R = NTAPS % 7 == 0 ? 7 : (NTAPS % 4 == 0 ? 4 : (NTAPS % 3 == 0 ? 3 : 1));
+  // (1x1: a 4-slot ring over the wave's chunks, the chunk loop unrolled by 4 so every slot is static)
+  static constexpr int R = NTAPS == 1 ? 4 : (NTAPS % 7 == 0 ? 7 : (NTAPS % 4 == 0 ? 4 : (NTAPS % 3 == 0 ? 3 : 1)));
   static constexpr int PD = R - 1;
   static_assert(R > 1, "tap count");
 };
@@ -170,11 +171,34 @@ __global__ __launch_bounds__(256, 1) void conv16s_kernel(const lic_conv_args a, 
 
   u32x4 fw[R][CT];
 #pragma unroll
-  for (int q = 0; q < PD; ++q) load_w(0, q, fw[q]);
+  for (int q = 0; q < PD; ++q) {   // the first PD steps: taps of chunk 0 (1x1: chunks 0 .. PD-1)
+    if constexpr (NTAPS == 1) load_w(q, 0, fw[q]);
+    else load_w(0, q, fw[q]);
+  }
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the halo; the first weights too)
   __syncthreads();
 
+  if constexpr (NTAPS == 1) {
+    // 1x1 (the slice loop's / hyper nets' Linears on 16x16 latents): one MFMA pair per chunk, the
+    // weights of chunk + PD in flight
+    for (int c0 = 0; c0 < ncw; c0 += R) {
+      c16_static_for<0, R>([&](auto uc) __attribute__((always_inline)) {
+        constexpr int u = decltype(uc)::value;
+        const int cidx = c0 + u;
+        if (cidx < ncw) {
+          load_w(cidx + PD, 0, fw[(u + PD) % R]);
+          const int hb0 = hlane[0] + chunk_of(cidx) * PLANE;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const u32x4 fbj = *(const u32x4*)(smem + hb0 + 2 * j * HWD * 32);
+#pragma unroll
+            for (int i = 0; i < CT; ++i) acc[i][j] = mfma_k16<T>(fw[u][i], fbj, acc[i][j]);
+          }
+        }
+      });
+    }
+  } else
   for (int cidx = 0; cidx < ncw; ++cidx) {
     const int kc = chunk_of(cidx);
     int hb[KW];

@@ -244,6 +244,11 @@ def test_gemm16_small_map_linear(dtype):
     (192, 192, 3, 3, 13, 21),     # ragged tiles (13 = 3*4+1 rows, 21 = 16+5 columns)
     (192, 192, 7, 5, 9, 30),      # ragged 7x7
     (128, 32, 3, 16, 16, 16),     # narrow output (one 32-channel block)
+    (128, 512, 1, 8, 16, 16),     # 1x1: slice-loop Swin MLP Linears (training batch), 64-channel blocks
+    (512, 128, 1, 8, 16, 16),     # 1x1: 32 input chunks over 4 waves
+    (64, 128, 1, 8, 16, 16),      # 1x1: ResidualUnit conv 64->128 (4 chunks: one per wave)
+    (240, 128, 1, 32, 16, 16),    # 1x1: SWAtten in_conv (15 chunks), the inference batch (8 K pixels)
+    (128, 64, 1, 3, 13, 21),      # 1x1: ragged tiles
 ])
 def test_conv16s_vs_torch_fp32(dtype, cin, cout, k, B, H, W):
     from lic_amd.layers import Conv2d
