@@ -52,7 +52,7 @@ def _env_int(k, d):
 PMC_FILES = {torch.float16: "profiles/r05/pmc_conv3x3_64_f16.json",
              torch.float32: "profiles/r02/pmc_conv3x3_64_f32.json",
              ("split", 1): "profiles/r02/pmc_conv3x3_64_f32x3.json",
-             ("split", 2): "profiles/r05/pmc_conv3x3_64_f32x6.json"}
+             ("split", 2): "profiles/r06/pmc_conv3x3_64_f32x6.json"}
 # the kernel that runs the roofline conv per precision (csrc/)
 ROOF_KERNEL = {0: "conv_halo_kernel", 1: "conv_halo_split_kernel", 2: "conv_split_wd_kernel"}
 # 16-bit activations run the roofline conv on csrc/conv16.h (round 5)
