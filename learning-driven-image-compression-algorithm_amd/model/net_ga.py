@@ -228,7 +228,7 @@ class analysisTransformModel(nn.Module):
         x = t[4].run(x)
         x = t[6].run(x, pad=(1, 1, 2, 2))     # ZeroPad2d((1, 2, 1, 2)) = left 1, right 2, top 1, bottom 2
         x = t[7].run(x)
-        x = t[8].run(x)
+        x = t[8].run(x, fork=fork and Fn.fork64_enabled())   # (64x64: conv_a beside conv_b, A/B)
         for i in (9, 10, 11):
             x = t[i].run(x)
         x = t[12].run(x)
@@ -278,7 +278,7 @@ class synthesisTransformModel(nn.Module):
         x = t[3].run(x)
         x = t[5].run(x, prepad=(1, 1))
         x = t[6].run(x)
-        x = t[7].run(x)
+        x = t[7].run(x, fork=Fn.fork64_enabled())   # (64x64: conv_a beside conv_b, A/B)
         x = t[9].run(x, prepad=(1, 1))
         x = t[10].run(x)
         x = t[12].run(x, prepad=(1, 1))
