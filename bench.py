@@ -49,7 +49,7 @@ def _env_int(k, d):
         return d
 
 
-PMC_FILES = {torch.float16: "profiles/r05/pmc_conv3x3_64_f16.json",
+PMC_FILES = {torch.float16: "profiles/r06/pmc_conv3x3_64_f16.json",
              torch.float32: "profiles/r02/pmc_conv3x3_64_f32.json",
              ("split", 1): "profiles/r02/pmc_conv3x3_64_f32x3.json",
              ("split", 2): "profiles/r06/pmc_conv3x3_64_f32x6.json"}
