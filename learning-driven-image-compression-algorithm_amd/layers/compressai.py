@@ -69,10 +69,25 @@ class ResidualBlockWithStride(nn.Module):
         self.gdn = GDN(out_ch)
         self.skip = conv1x1(in_ch, out_ch, stride=stride) if (stride != 1 or in_ch != out_ch) else None
 
-    def run(self, x: Act, out: Optional[Act] = None) -> Act:
+    def run(self, x: Act, out: Optional[Act] = None, fork: bool = False) -> Act:
+        """fork=True (called on the capture stream) and LIC_FORK_SKIP=1: the 1x1 s2 skip on a side stream
+        forked from the current one (a sibling of every other fork, never nested), beside conv1 -> conv2;
+        joined before the GDN epilogue that adds it.  Same launches, same arithmetic; opt-in because it
+        measured neutral (fp32x6 1075.6 / 1074.3 -> 1073.9 / 1076.6 images/s, profiles/r06/fork_skip_ab.txt)."""
+        side = None
+        if fork and self.skip is not None and Fn.fork_enabled() and os.environ.get("LIC_FORK_SKIP", "0") == "1":
+            main = torch.cuda.current_stream(x.t.device)
+            side = Fn.aux_stream(x.t.device, "skip")
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                identity = self.skip.run(x)
         t = self.conv1.run(x, act=ACT_LRELU)
         t = self.conv2.run(t)
-        identity = self.skip.run(x) if self.skip is not None else x
+        if side is not None:
+            main.wait_stream(side)
+            identity.t.record_stream(main)   # allocated on the side stream, read by the GDN launch here
+        else:
+            identity = self.skip.run(x) if self.skip is not None else x
         return self.gdn.run(t, out, r1=identity)
 
     def forward(self, x):

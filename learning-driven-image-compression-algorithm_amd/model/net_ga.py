@@ -224,14 +224,14 @@ class analysisTransformModel(nn.Module):
         else:
             for i in range(3):
                 x = t[i].run(x)
-        x = t[3].run(x)
+        x = t[3].run(x, fork=fork)   # (the 1x1 s2 skip beside conv1 -> conv2)
         x = t[4].run(x)
         x = t[6].run(x, pad=(1, 1, 2, 2))     # ZeroPad2d((1, 2, 1, 2)) = left 1, right 2, top 1, bottom 2
         x = t[7].run(x)
         x = t[8].run(x, fork=fork and Fn.fork64_enabled())   # (64x64: conv_a beside conv_b, A/B)
         for i in (9, 10, 11):
             x = t[i].run(x)
-        x = t[12].run(x)
+        x = t[12].run(x, fork=fork)
         x = t[13].run(x)
         x = t[15].run(x, pad=(1, 1, 2, 2))
         return t[16].run(x, out, fork=fork)   # (the 16x16 latents: conv_a concurrent with conv_b)
