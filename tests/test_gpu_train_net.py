@@ -341,3 +341,76 @@ def test_train_step_hipgraph_matches_eager():
     d, d_ee = dmax(net_a, net_b), dmax(net_a, net_a2)
     print(f"[train hipGraph] max relative parameter difference graph-eager {d:.2e}, eager-eager {d_ee:.2e}")
     assert d == 0 and d_ee == 0
+
+
+def test_train_step_frozen_deferred_matches_plain():
+    """train_net_unet.py's one-GPU step: the parameters the optimiser does not own (the slice-loop
+    modules the reference leaves out of base_params) take no weight gradient, and the backward's
+    split-K wgrad reduces run as one batched launch (autograd.WgradDefer).  Neither changes a bit of
+    what the optimiser sees: 3 steps of that setup -- eager, and captured + replayed with the
+    descriptor table filled after the capture -- give the same losses and parameters as the plain
+    eager steps."""
+    import contextlib
+    import copy
+    from lic_amd import autograd as AG
+    from lic_amd.model import net_unet_ha_hs, net_ga
+    torch.manual_seed(0)
+    base = net_ga.synthetic_syntax_bias_(net_unet_ha_hs.Net((1, 256, 256, 3), (1, 256, 256, 3), False, False,
+                                                            precision="bf16"))
+    x = (torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(9)) * 2 - 1).to(DEV)
+    lmbda, steps = 0.0025, 3
+
+    def make(frozen):
+        net = copy.deepcopy(base).to(DEV)
+        params = net.base_params()
+        if frozen:
+            ids = {id(p) for p in params}
+            for p in net.parameters():
+                if id(p) not in ids:
+                    p.requires_grad_(False)
+        opt = torch.optim.Adam(params, lr=torch.tensor(1e-4, device=DEV), capturable=True)
+        return net, params, opt, torch.zeros((1,), dtype=torch.int64, device=DEV)
+
+    def body(net, params, opt, seed_t, defer):
+        bpp, mse = net(x, "train", seed_dev=seed_t)
+        loss = lmbda * 255 ** 2 * mse + bpp
+        with defer if defer is not None else contextlib.nullcontext():
+            loss.backward()
+        torch.nn.utils.clip_grad_norm_([p for p in params if p.grad is not None], 1.0)
+        opt.step()
+        seed_t.add_(1)
+        return loss.detach()
+
+    def eager(frozen, defer):
+        net, p, o, s = make(frozen)
+        losses = []
+        for _ in range(steps):
+            o.zero_grad(set_to_none=True)
+            losses.append(body(net, p, o, s, defer).item())
+        return net, losses
+
+    net_plain, l_plain = eager(False, None)
+    net_fd, l_fd = eager(True, AG.WgradDefer())
+    d = AG.WgradDefer()
+    net_g, pg, og, sg = make(True)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        og.zero_grad(set_to_none=True)
+        first = body(net_g, pg, og, sg, d).item()            # eager warm-up = step 1 (sizes the table)
+    torch.cuda.current_stream().wait_stream(side)
+    og.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        out = body(net_g, pg, og, sg, d)
+    d.finalize()
+    l_g = [first]
+    for _ in range(steps - 1):
+        g.replay()
+        l_g.append(out.item())
+    torch.cuda.synchronize()
+    print(f"\n[frozen + deferred] plain {l_plain}, eager {l_fd}, graph {l_g}")
+    assert l_plain == l_fd == l_g
+    for m in (net_fd, net_g):
+        for (n, p), q in zip(net_plain.named_parameters(), m.parameters()):
+            assert torch.equal(p, q), n
