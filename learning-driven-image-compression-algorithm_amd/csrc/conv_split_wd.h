@@ -40,6 +40,13 @@
 #ifndef WD_ALT
 #define WD_ALT 1
 #endif
+// two-slot B rings (R = 2): each weight part of step s + 2 is loaded right after this step's last product
+// that reads the part (w2 after the 3rd product, w1 after the 5th, w0 after the 6th) into the slot it
+// frees, instead of all parts of step s + 1 at the top of the step: the same registers, up to two steps
+// of latency (0: the old order, A/B)
+#ifndef WD_LATE_B
+#define WD_LATE_B 1
+#endif
 
 namespace lic {
 
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
   u32x4 fa[NPA][TM];
   // one tap's products; the running sum is the MFMA's C operand.  `mid` runs after the first product
   // group: the next chunk's split work of this step, interleaved with the MFMAs by the scheduler
-  auto step = [&](const char* set, int toff_next, bool has_next, const u32x4(&fbc)[NPB][TN], auto&& mid) {
+  auto step = [&](const char* set, int toff_next, bool has_next, u32x4(&fbc)[NPB][TN], auto&& mid, auto&& after_b) {
 #pragma unroll
     for (int pr = NPROD - 1; pr >= 0; --pr) {
 #pragma unroll
@@ -329,6 +336,10 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
 #if !(WD_ABL & 4)
       if (has_next && last) load_a_part(set, toff_next, SM::PA[pr], fa);
 #endif
+      bool last_b = true;   // the last product of this tap reading weight part PB[pr] (compile-time)
+#pragma unroll
+      for (int q = 0; q < pr; ++q) last_b = last_b && SM::PB[q] != SM::PB[pr];
+      if (last_b) after_b(SM::PB[pr]);
       if (pr == NPROD - 1) mid();
 #if WD_SB
       __builtin_amdgcn_sched_barrier(0);
@@ -362,8 +373,24 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
     u32x4 fb[R][NPB][TN];
     // the pack's step index of the group's step tl (compile-time) of chunk k (tl may run past the chunk)
     auto gstep = [&](int k, int tl) { return (k + tl / NTG) * NTAPS + T0 + tl % NTG; };
+    constexpr bool LATE = WD_LATE_B && R == 2 && !(WD_ABL & 2);   // (R = 2: PD = 1)
+    // one weight part of step s (clamped) into slot fb_s: n-tiles as load_b
+    auto load_b_part = [&](int s, int pl, u32x4(&fbs)[NPB][TN]) {
+      s = s < nsteps ? s : nsteps - 1;
 #pragma unroll
-    for (int q = 0; q < PD; ++q) load_b(gstep(0, q), fb[q]);
+      for (int j = 0; j < TN; ++j) {
+        int jt = n0 / 32 + wn * TN + j;
+        jt = jt < ntiles ? jt : ntiles - 1;
+        fbs[pl][j] = __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, ((jt * nsteps + s) * NPB + pl) * 1024, 0);
+      }
+    };
+    if constexpr (LATE) {
+      load_b(gstep(0, 0), fb[0]);
+      load_b(gstep(0, 1), fb[1]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < PD; ++q) load_b(gstep(0, q), fb[q]);
+    }
     __syncthreads();
 
     // one chunk; KSI = chunk index mod KU (compile-time), so the group's step (k, tl) sits in ring slot
@@ -411,7 +438,7 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
         // kept in this order by the scheduling barriers: the prefetches are issued before this
         // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
 #if !(WD_ABL & 2)
-        load_b(gstep(k, tl + PD), fb[(sr + PD) % R]);
+        if constexpr (!LATE) load_b(gstep(k, tl + PD), fb[(sr + PD) % R]);
 #endif
         if constexpr (FIX) {
           toff = T0 + tl + 1;
@@ -423,7 +450,8 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        step(set, toff, tl + 1 < NTG, fb[sr % R], [&]() {
+        auto& fbs = fb[sr % R];
+        step(set, toff, tl + 1 < NTG, fbs, [&]() {
 #if !(WD_ABL & 1)
 #pragma unroll
           for (int i = tl * QPS; i < (tl + 1) * QPS && i < NQ; ++i) {
@@ -435,6 +463,9 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
 #endif
           }
 #endif
+        }, [&](int pl) {
+          // slot sr % 2 held this step's part pl; step sr + 2 uses the same slot
+          if constexpr (LATE) load_b_part(gstep(k, tl + 2), pl, fbs);
         });
         __builtin_amdgcn_sched_barrier(0);
       }
