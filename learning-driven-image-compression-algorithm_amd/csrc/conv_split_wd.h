@@ -47,6 +47,12 @@
 #ifndef WD_LATE_B
 #define WD_LATE_B 1
 #endif
+// with WD_LATE_B: part 0 (read first in a step, last used by its final product) gets a third slot and is
+// loaded two steps ahead at the top of each step, where the step count per loop trip allows a static slot
+// (measured neutral, r06u: 3x3 @64^2 353.5 -> 355.3 us, off)
+#ifndef WD_W0R3
+#define WD_W0R3 0
+#endif
 
 namespace lic {
 
@@ -317,17 +323,21 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
   u32x4 fa[NPA][TM];
   // one tap's products; the running sum is the MFMA's C operand.  `mid` runs after the first product
   // group: the next chunk's split work of this step, interleaved with the MFMAs by the scheduler
-  auto step = [&](const char* set, int toff_next, bool has_next, u32x4(&fbc)[NPB][TN], auto&& mid, auto&& after_b) {
+  // fb0c: part 0's slot when it has its own ring (w0r3), else unused (fbc[0] holds part 0)
+  auto step = [&](const char* set, int toff_next, bool has_next, u32x4(&fbc)[NPB][TN], const u32x4(&fb0c)[TN],
+                  auto w0r3, auto&& mid, auto&& after_b) {
+    constexpr bool W0 = decltype(w0r3)::value;
 #pragma unroll
     for (int pr = NPROD - 1; pr >= 0; --pr) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
+          const u32x4& bop = (W0 && SM::PB[pr] == 0) ? fb0c[j] : fbc[SM::PB[pr]][j];
 #if WD_ABL & 16
-          acc[i][j][0] += __uint_as_float(fa[SM::PA[pr]][i][0] ^ fbc[SM::PB[pr]][j][0]);
+          acc[i][j][0] += __uint_as_float(fa[SM::PA[pr]][i][0] ^ bop[0]);
 #else
-          acc[i][j] = mfma_k16<T>(fa[SM::PA[pr]][i], fbc[SM::PB[pr]][j], acc[i][j]);
+          acc[i][j] = mfma_k16<T>(fa[SM::PA[pr]][i], bop, acc[i][j]);
 #endif
         }
       bool last = true;   // the last product of this tap reading part PA[pr] (folded at compile time)
@@ -384,7 +394,18 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
         fbs[pl][j] = __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, ((jt * nsteps + s) * NPB + pl) * 1024, 0);
       }
     };
-    if constexpr (LATE) {
+    constexpr bool W0R3 = LATE && WD_W0R3 && (KU * NTG) % 3 == 0 && NQ <= 4;   // (NQ 6: 12 more registers spill)
+    u32x4 fb0[W0R3 ? 3 : 1][TN];
+    if constexpr (W0R3) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        load_b_part(gstep(0, q), 0, fb[q]);   // (slot's part 0 unused; only fills the registers' shape)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb0[q][j] = fb[q][0][j];
+        load_b_part(gstep(0, q), 1, fb[q]);
+        load_b_part(gstep(0, q), 2, fb[q]);
+      }
+    } else if constexpr (LATE) {
       load_b(gstep(0, 0), fb[0]);
       load_b(gstep(0, 1), fb[1]);
     } else {
@@ -439,6 +460,16 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
         // step's MFMAs (left to itself the scheduler sinks them next to their consumers)
 #if !(WD_ABL & 2)
         if constexpr (!LATE) load_b(gstep(k, tl + PD), fb[(sr + PD) % R]);
+        if constexpr (W0R3) {   // part 0 of step + 2 into the slot step - 1 freed
+          u32x4(&d0)[TN] = fb0[(sr + 2) % 3];
+          const int s2 = gstep(k, tl + 2) < nsteps ? gstep(k, tl + 2) : nsteps - 1;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            int jt = n0 / 32 + wn * TN + j;
+            jt = jt < ntiles ? jt : ntiles - 1;
+            d0[j] = __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, ((jt * nsteps + s2) * NPB + 0) * 1024, 0);
+          }
+        }
 #endif
         if constexpr (FIX) {
           toff = T0 + tl + 1;
@@ -451,7 +482,7 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
         }
         __builtin_amdgcn_sched_barrier(0);
         auto& fbs = fb[sr % R];
-        step(set, toff, tl + 1 < NTG, fbs, [&]() {
+        step(set, toff, tl + 1 < NTG, fbs, fb0[W0R3 ? sr % 3 : 0], std::integral_constant<bool, W0R3>{}, [&]() {
 #if !(WD_ABL & 1)
 #pragma unroll
           for (int i = tl * QPS; i < (tl + 1) * QPS && i < NQ; ++i) {
@@ -465,7 +496,9 @@ __global__ __launch_bounds__(KS * WM * WN * 64, OCC > 0 ? OCC : ((TH * TW / WM =
 #endif
         }, [&](int pl) {
           // slot sr % 2 held this step's part pl; step sr + 2 uses the same slot
-          if constexpr (LATE) load_b_part(gstep(k, tl + 2), pl, fbs);
+          if constexpr (LATE) {
+            if (!(W0R3 && pl == 0)) load_b_part(gstep(k, tl + 2), pl, fbs);
+          }
         });
         __builtin_amdgcn_sched_barrier(0);
       }
