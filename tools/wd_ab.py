@@ -6,7 +6,7 @@ Times the a_model's big-map fp32x6 convs with HIP events on the launch stream an
 outputs; with --ref FILE it also checks that this run's outputs are bitwise equal to FILE's (a
 retiling keeps every output element's chunk / tap / product sequence, so A and B must agree bit
 for bit).
-usage: python tools/wd_ab.py --save gpurun_out/a.pt; LIC_WD_W4=1 python tools/wd_ab.py --ref gpurun_out/a.pt
+usage: python tools/wd_ab.py [--small] --save /tmp/a.pt; LIC_LIB=<variant .so> python tools/wd_ab.py [--small] --ref /tmp/a.pt
 """
 import argparse
 import os
@@ -24,6 +24,15 @@ SHAPES = [
     ("conv5x5s2@128", 192, 192, 5, 2, (1, 1, 2, 2), 128),
     ("rbws3x3s2@64", 192, 192, 3, 2, (1, 1, 1, 1), 64),
 ]
+# --small: the latent-map launches (8 x 8-pixel tiles, tap groups)
+SMALL = [
+    ("wnsa3x3@16", 192, 192, 3, 1, (1, 1, 1, 1), 16),
+    ("cc3x3_224_128@16", 224, 128, 3, 1, (1, 1, 1, 1), 16),
+    ("cc3x3_128_48@16", 128, 48, 3, 1, (1, 1, 1, 1), 16),
+    ("ru3x3_64@16", 64, 64, 3, 1, (1, 1, 1, 1), 16),
+    ("wnsa7x7@16", 192, 192, 7, 1, (3, 3, 3, 3), 16),
+    ("lin128_512@16", 128, 512, 1, 1, (0, 0, 0, 0), 16),
+]
 PEAK6 = 2516.6 / 6
 
 
@@ -34,6 +43,7 @@ def main():
     ap.add_argument("--save", default="")
     ap.add_argument("--ref", default="")
     ap.add_argument("--only", default="")
+    ap.add_argument("--small", action="store_true", help="the latent-map shapes instead")
     args = ap.parse_args()
     import lic_amd.functional as Fn
     from lic_amd.layers import Conv2d
@@ -42,7 +52,7 @@ def main():
     st = torch.cuda.current_stream()
     ref = torch.load(args.ref, weights_only=True) if args.ref else {}
     outs, bad = {}, 0
-    for name, ci, co, k, s, pad, H in SHAPES:
+    for name, ci, co, k, s, pad, H in (SMALL if args.small else SHAPES):
         if args.only and name not in args.only.split(","):
             continue
         torch.manual_seed(0)
